@@ -1,0 +1,193 @@
+#!/usr/bin/env python3
+"""UNet denoising steps/sec (T=8, 4x64x64 latent) on MI355X — BASELINE.json's headline metric.
+
+One "step" = one denoising step of the reference sampler (trainers_ldm_cond.py:1130-1166)
+on one T=8 clip: the SD-1.4 UNet forward over B=8 frames of [x_t || rgb] (8x64x64,
+cross-attention removed, 815.5 M params, random init) + one fused DDIM step, replayed as
+one captured HIP graph per step.  Frames are independent (no temporal layers),
+so N GPUs run N independent clips: no collective on the data path, weak scaling;
+``value`` = N x K steps / max-over-ranks wall time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  It carries a "roofline" object for the dominant kernel
+family (HIP events around every launch of an instrumented step, algorithmic FLOPs/bytes)
+and, at N=1, a "cpu_baseline" timed on the host cores with the oracle restatement.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "video-latent-diffusion-panoptic-segmentation_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "UNet denoising steps/sec (T=8, 4×64×64 latent)"
+PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_FP32_TFLOPS = 157.3      # fp32 MFMA = vector rate
+PEAK_HBM_GBS = 8000.0
+
+
+def build_unet(dev, dtype):
+    from ldmseg.models import UNet
+    torch.manual_seed(0)
+    with torch.device(dev):
+        u = UNet()                                        # SD-1.4 UNet2DConditionModel config
+    u.remove_cross_attention()                            # base.yaml:71 image_descriptors: remove
+    u.modify_encoder(in_channels=8, init_mode_seg="copy", init_mode_image="zero")   # base.yaml:37-45
+    return u.to(dtype=dtype).eval()
+
+
+def make_scheduler(dev):
+    from ldmseg.schedulers import DDIMNoiseScheduler
+    s = DDIMNoiseScheduler(prediction_type="epsilon", beta_schedule="scaled_linear", num_train_timesteps=1000,
+                           beta_start=0.00085, beta_end=0.012, steps_offset=1, clip_sample=False,
+                           set_alpha_to_one=False, device=dev, verbose=False)          # base.yaml:48-62
+    s.set_timesteps_inference(50)
+    return s
+
+
+def roofline(unet, stepper, ts, nsteps, dtype):
+    from ldmseg.ops import native as K
+    prof = K.LaunchProfiler()
+    K.set_profiler(prof)
+    try:
+        for i in range(nsteps):
+            t = ts[i % len(ts)]
+            stepper.t_int.copy_(stepper._ar[t:t + 1])
+            stepper.t_f.copy_(stepper._arf[t:t + 1])
+            stepper._body()
+    finally:
+        K.set_profiler(None)
+    fam = prof.summary()
+    per_step = {k: dict(launches=v["launches"] // nsteps, ms=round(v["ms"] / nsteps, 4),
+                        gflop=round(v["flops"] / nsteps / 1e9, 2), mb=round(v["bytes"] / nsteps / 1e6, 2))
+                for k, v in fam.items()}
+    dom = max(fam, key=lambda k: fam[k]["ms"])
+    d = fam[dom]
+    if d["flops"] > 0:
+        achieved = d["flops"] / (d["ms"] * 1e-3) / 1e12
+        peak = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_FP32_TFLOPS
+        rl = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 1), "peak": peak, "unit": "TFLOP/s",
+              "frac": round(achieved / peak, 4)}
+    else:
+        achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+        rl = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+              "frac": round(achieved / PEAK_HBM_GBS, 4)}
+    rl["traffic"] = None
+    rl["avg_launch_ms"] = round(d["ms"] / d["launches"], 5)
+    rl["algorithmic_per_launch"] = round((d["flops"] or d["bytes"]) / d["launches"], 1)
+    rl["kernels_per_step"] = per_step
+    return rl
+
+
+def cpu_baseline(unet, budget_s=25.0):
+    """Oracle restatement (oracle/unet.py + oracle/ddim.py, fp32 torch on the host cores),
+    bounded sample: whole frames of the T=8 step until ~budget_s, scaled to steps/s."""
+    from oracle import ddim as oddim
+    from oracle import unet as ounet
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    torch.set_num_threads(threads)
+    sd = {k: v.detach().float().cpu() for k, v in unet.state_dict().items()}
+    cfg = dict(unet.config)
+    _, ac, final = oddim.tables("scaled_linear", 1000, 0.00085, 0.012, False)
+    g = torch.Generator().manual_seed(5)
+    frames, elapsed = 0, 0.0
+    with torch.no_grad():
+        while elapsed < budget_s and frames < 8:
+            x = torch.randn(1, 4, 64, 64, generator=g)
+            rgb = torch.randn(1, 4, 64, 64, generator=g)
+            t0 = time.perf_counter()
+            eps = ounet.forward(sd, cfg, torch.cat([x, rgb], 1), torch.tensor(979))
+            oddim.step(ac, final, 1000, 50, eps, 979, x)
+            elapsed += time.perf_counter() - t0
+            frames += 1
+    per_step = elapsed / frames * 8
+    return {"value": round(1.0 / per_step, 5), "unit": "steps/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} frame(s) of one T=8 denoising step (UNet fwd + DDIM, fp32, 64x64), "
+                      f"{elapsed:.1f} s, scaled x{8 / frames:g} to one 8-frame step"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--frames", type=int, default=8, help="T: frames per clip (folded into the batch)")
+    ap.add_argument("--latent", type=int, default=64)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-steps", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)   # RCCL; used only for barrier + timing reduce
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+
+    from ldmseg.pipelines import DenoiseStep
+    unet = build_unet(dev, dtype)
+    sched = make_scheduler(dev)
+    B, L = args.frames, args.latent
+    g = torch.Generator().manual_seed(1 + rank)                    # each rank: its own clip
+    rgb = torch.randn(B, 4, L, L, generator=g).to(dev)
+    stepper = DenoiseStep(unet, sched, rgb, self_condition=False, use_graph=not args.no_graph)
+    stepper.set_latents(torch.randn(B, 4, L, L, generator=g).to(dev))
+    ts = [int(t) for t in sched.timesteps]
+
+    for i in range(args.warmup):
+        stepper.run(ts[i % len(ts)], last=False)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        stepper.run(ts[k % len(ts)], last=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = te.item()
+    finite = bool(torch.isfinite(stepper.lat).all().item())
+
+    rl = roofline(unet, stepper, ts, args.profile_steps, dtype) if rank == 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(unet)
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(world * args.steps / elapsed, 4), "unit": "steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic: random-init SD-1.4 UNet weights, N(0,1) KITTI-shaped 4x64x64 latents",
+            "config": {"workload": f"UNet fwd (B={B} frames = one T={B} clip, 8x{L}x{L} input) + DDIM step, "
+                                   "HIP graph per step",
+                       "model": "SD-1.4 UNet2DConditionModel, cross-attn removed, 8-ch conv_in (815.5M)",
+                       "global_batch": B * world, "seq_len": L * L,
+                       "parallelism": f"replicas x{world} (independent clips, no data-path collective)"},
+            "outputs_finite": finite,
+            "roofline": rl,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

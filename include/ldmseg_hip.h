@@ -1,0 +1,198 @@
+/*
+ * ldmseg_hip.h — C ABI of the MI355X (gfx950) kernels behind the latent-diffusion
+ * denoising path of weentiaan/Video-latent-diffusion-panoptic-segmentation.
+ *
+ * The reference has no FFI: its hot path is the nn.Module / scheduler Python API, whose
+ * arithmetic is dispatched implicitly to stock PyTorch / diffusers kernels.
+ * Each entry point below replaces one family of those implicit op sites; the drop-in
+ * Python modules (ldmseg.models.UNet / GeneralVAESeg, ldmseg.schedulers.DDIMNoiseScheduler)
+ * bind them with ctypes.
+ *
+ * Conventions
+ *  - All pointers are DEVICE pointers owned by the caller (PyTorch caching allocator); no
+ *    entry point allocates, frees or synchronises, so every call is hipGraph-capturable.
+ *  - Activations inside the UNet/VAE are NHWC ("rows" = pixels or tokens, channels
+ *    contiguous).  Boundary tensors (UNet sample/output, VAE input/logits) are NCHW.
+ *  - dtype codes: LDM_F32 (exact fp32 path, the 1e-3 parity gate) or LDM_BF16 (fp32
+ *    accumulation, bf16 storage — the performance path).
+ *  - Return value: LDM_OK or an LDM_ERR_* code (ldm_status_string() describes it); shape
+ *    and alignment preconditions are checked on the host before any launch.
+ */
+#ifndef LDMSEG_HIP_H
+#define LDMSEG_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* ldm_stream_t; /* == hipStream_t */
+
+enum { LDM_F32 = 0, LDM_BF16 = 1 };
+enum {
+  LDM_OK = 0,
+  LDM_ERR_ARG = 1,     /* bad argument / unsupported configuration */
+  LDM_ERR_ALIGN = 2,   /* pointer or channel count violates the vector-width requirement */
+  LDM_ERR_LAUNCH = 3,  /* hipLaunchKernel failed */
+};
+
+/* ---------------------------------------------------------------------------------------
+ * ldm_conv2d — implicit-GEMM convolution / GEMM on MFMA.
+ * Replaces: every nn.Conv2d (3x3 stride 1/2, 1x1), nn.Linear and ConvTranspose2d(k2,s2)
+ * site of the path — diffusers ResnetBlock2D conv1/conv2/conv_shortcut, Transformer2DModel
+ * proj_in/proj_out, Attention to_q/k/v/to_out, FeedForward GEGLU + net.2,
+ * TimestepEmbedding linear_1/2, time_emb_proj, Down/Upsample2D conv
+ * (reached via ldmseg/models/unet.py:305-307,357,361-431) and GeneralVAESeg encoder/decoder
+ * convs (ldmseg/models/vae.py:134-173,191-245).
+ *
+ *   out[m, n] = epilogue( sum_k A[m, k] * W[n, k] )
+ * A rows m = (b, oy, ox) over batch x h_out x w_out; k = (ky, kx, c) tap-major over the
+ * channel concatenation [a0 (c0 ch) || a1 (c1 ch)] of the NHWC input, zero padded by
+ * ksize/2 (optionally read through a nearest-2x upsample, Upsample2D).
+ * W is pre-packed [n_alloc][kpad] (K = ksize*ksize*(c0+c1) padded with zeros to kpad).
+ * ------------------------------------------------------------------------------------- */
+enum { LDM_OUT_NHWC = 0, LDM_OUT_NCHW = 1, LDM_OUT_GEGLU = 2, LDM_OUT_SHUFFLE2 = 3 };
+enum { LDM_ACT_NONE = 0, LDM_ACT_SILU = 1 };
+
+typedef struct {
+  const void* a0;          /* NHWC [batch][h_in][w_in][c0] */
+  const void* a1;          /* NHWC [batch][h_in][w_in][c1] or NULL (c1 == 0) */
+  int c0, c1;
+  int batch, h_in, w_in;
+  int h_out, w_out;
+  int ksize;               /* 1 or 3 */
+  int stride;              /* 1 or 2 */
+  int upsample;            /* 1: input is nearest-upsampled x2 before the conv */
+  const void* w;           /* [n_alloc][kpad] */
+  int n;                   /* GEMM N (for GEGLU: 2 x output channels, for SHUFFLE2: 4 x Cout) */
+  int kpad;                /* multiple of 64 */
+  const float* bias;       /* [n] or NULL (packed like W for GEGLU / SHUFFLE2) */
+  const float* temb;       /* per-(batch, n) additive term: temb[b * temb_stride + n], or NULL */
+  int temb_stride;
+  const void* residual;    /* same layout/dtype as out, added after activation; may alias out */
+  void* out;
+  int out_layout;          /* LDM_OUT_* */
+  int act;                 /* LDM_ACT_* applied after bias/temb, before residual */
+  int dtype;               /* A / W / residual dtype */
+  int out_f32;             /* 1: out is fp32 regardless of dtype */
+} ldm_conv_params;
+
+int ldm_conv2d(const ldm_conv_params* p, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).
+ * Replaces: diffusers Attention(AttnProcessor) self-attention attn1 (and cross-attention
+ * attn2 when not removed, unet.py:83-105): softmax(Q K^T * scale) V per (batch, head).
+ * Row r of batch b, head h lives at ptr + (b * n + r) * stride + h * head_dim.
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+  const void* q; const void* k; const void* v; void* o;
+  int q_stride, k_stride, v_stride, o_stride;  /* elements between consecutive rows */
+  int batch, heads, head_dim;                   /* head_dim <= 160 */
+  int n_q, n_kv;
+  float scale;
+  int dtype;
+} ldm_attn_params;
+
+int ldm_attention(const ldm_attn_params* p, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * ldm_group_norm — GroupNorm (+ optional SiLU) over NHWC rows of one or two channel-
+ * concatenated sources (the up-block [hidden || skip] concat is never materialised).
+ * Replaces: ResnetBlock2D norm1/norm2 + SiLU (eps 1e-5), Transformer2DModel.norm (eps 1e-6),
+ * conv_norm_out + conv_act (unet.py:428-430), GeneralVAESeg GroupNorm (vae.py:163,235).
+ * workspace: >= ldm_group_norm_workspace_bytes(batch, hw, c0 + c1) bytes of device memory.
+ * ------------------------------------------------------------------------------------- */
+size_t ldm_group_norm_workspace_bytes(int batch, int hw, int channels);
+int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
+                   const float* gamma, const float* beta, float eps, int act, void* out,
+                   void* workspace, int dtype, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * ldm_layer_norm — LayerNorm over the channel dimension of [rows][c] (NHWC pixels or tokens).
+ * Replaces: BasicTransformerBlock norm1/norm2/norm3 (eps 1e-5) and LayerNorm2d
+ * (vae.py:310-323, eps 1e-6), optionally followed by SiLU (vae.py:158).
+ * ------------------------------------------------------------------------------------- */
+int ldm_layer_norm(const void* x, int rows, int c, const float* gamma, const float* beta,
+                   float eps, int act, void* out, int dtype, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * ldm_timestep_proj — sinusoidal timestep projection (diffusers Timesteps, unet.py:305):
+ * out[b, :] = flip? [cos(t_b f) || sin(t_b f)] : [sin || cos],  f = freqs[0..dim/2).
+ * t is read on the device (fp32 [n_t], n_t == 1 broadcasts over batch: unet.py:303), so
+ * the DDIM loop never syncs to the host.
+ * ------------------------------------------------------------------------------------- */
+int ldm_timestep_proj(const float* t, int n_t, int batch, const float* freqs, int dim,
+                      int flip_sin_to_cos, void* out, int dtype, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * ldm_ddim_step — fused DDIM reverse step (ldmseg/schedulers/ddim_scheduler.py:218-269).
+ * Coefficients are derived on the device from t (int64, device) and the alphas_cumprod
+ * table (fp32, device), so a device-resident timestep costs no host sync (the reference
+ * indexes a CPU table with a device scalar every step).
+ * Tensors: model_output (mo_dtype), sample (x_dtype) -> prev, x0 (out_dtype); n elements.
+ * ------------------------------------------------------------------------------------- */
+enum { LDM_PRED_EPSILON = 0, LDM_PRED_SAMPLE = 1, LDM_PRED_V = 2 };
+typedef struct {
+  const void* model_output; int mo_dtype;
+  const void* sample; int x_dtype;
+  void* prev; void* x0; int out_dtype;   /* either may be NULL */
+  int64_t n;
+  const int64_t* t;                      /* device scalar */
+  const float* alphas_cumprod;           /* device [num_train_timesteps] */
+  float final_alpha_cumprod;
+  int step_ratio;                        /* num_train_timesteps // num_inference_steps */
+  int prediction_type;
+  int clip_sample; float clip_range;
+  int use_clipped_model_output;
+  int num_train_timesteps;               /* table length; an out-of-range t yields NaN, never an OOB read */
+} ldm_ddim_step_params;
+
+int ldm_ddim_step(const ldm_ddim_step_params* p, ldm_stream_t stream);
+
+/* add_noise (:155-187) / remove_noise (:189-216): per-sample timesteps t[batch], device. */
+int ldm_ddim_add_noise(const void* x0, const void* noise, const int64_t* t, const float* alphas_cumprod,
+                       int num_train_timesteps, float scale, int batch, int64_t per_sample, void* out,
+                       int dtype, ldm_stream_t stream);
+int ldm_ddim_remove_noise(const void* xt, const void* noise, const int64_t* t, const float* alphas_cumprod,
+                          int num_train_timesteps, float scale, int batch, int64_t per_sample, void* out,
+                          int dtype, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Bit-channel mask codec (bit-exact). Replaces Cityscapes/KITTI encode_bitmap /
+ * decode_bitmap (ldmseg/data/cityscapes.py:256-270, kitti.py:292-306, coco.py:378-391).
+ * encode: ids int64 [batch][hw] -> planes fp32 [batch][n][hw] (+ ignore mask uint8 [batch][hw])
+ * decode: planes [batch][n][hw] (dtype) -> ids int64 [batch][hw]; drop_31: v == 31 -> 0.
+ * ------------------------------------------------------------------------------------- */
+int ldm_bit_encode(const int64_t* ids, int batch, int64_t hw, int n, int64_t ignore_label,
+                   float fill_value, float* planes, uint8_t* ignore_mask, ldm_stream_t stream);
+int ldm_bit_decode(const void* planes, int batch, int n, int64_t hw, int drop_31, int64_t* ids,
+                   int dtype, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Layout / resampling helpers on the path boundary.
+ * ldm_nchw_to_nhwc: gathers up to 3 NCHW sources (the sampler's [x_t || rgb || cond] concat,
+ * trainers_ldm_cond.py:1134-1141) into one NHWC tensor with c_pad channels (zero filled).
+ * ldm_resize_bilinear: F.interpolate(mode='bilinear', align_corners=False) on NCHW
+ * (vae.py:271, trainers_ldm_cond.py:343,380-392); optional affine y = x*mul + add.
+ * ldm_gaussian_posterior: DiagonalGaussianDistribution (vae.py:371-415) from NHWC moments.
+ * ------------------------------------------------------------------------------------- */
+int ldm_nchw_to_nhwc(const void* s0, int c0, int dt0, const void* s1, int c1, int dt1,
+                     const void* s2, int c2, int dt2, int batch, int hw, int c_pad,
+                     void* out, int dtype, ldm_stream_t stream);
+int ldm_resize_bilinear(const void* x, int planes, int h_in, int w_in, int h_out, int w_out,
+                        float scale_h, float scale_w, float mul, float add, void* out,
+                        int in_dtype, int out_dtype, ldm_stream_t stream);
+enum { LDM_POST_NONE = 0, LDM_POST_TANH = 1, LDM_POST_SIGMOID = 2, LDM_POST_CLIP = 3 };
+int ldm_gaussian_posterior(const void* moments, int batch, int hw, int latent_channels,
+                           int clamp_output, int act_fn, float* mean, float* logvar, float* std,
+                           float* var, int dtype, ldm_stream_t stream);
+
+const char* ldm_status_string(int status);
+int ldm_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LDMSEG_HIP_H */

@@ -1,0 +1,272 @@
+"""Per-op parity of the HIP kernels (through the C ABI) on an MI355X.
+
+References: the reference's golden vectors where the op is the reference's (DDIM, codec),
+otherwise plain torch fp32 on the CPU (floating-point kernels).
+Tolerances (stated per test): fp32 path 1e-4 relative to the tensor scale (exact fp32 MFMA,
+only summation order differs); bf16 path 2e-2 (8-bit mantissa storage, fp32 accumulate).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from golden_utils import DDIM_CONFIGS, load
+from ldmseg.ops import native as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel_err(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def tol(dt):
+    return 1e-4 if dt == torch.float32 else 2e-2
+
+
+DTYPES = [torch.float32, torch.bfloat16]
+
+
+# ------------------------------------------------------------------------------ conv / gemm
+CONV_CASES = [
+    # name, B, Cin(a0), Cin(a1), H, W, Cout, k, stride, upsample
+    ("3x3", 2, 64, 0, 16, 12, 96, 3, 1, False),
+    ("3x3_s2", 2, 64, 0, 15, 17, 64, 3, 2, False),
+    ("3x3_up", 1, 128, 0, 8, 6, 64, 3, 1, True),
+    ("3x3_concat", 2, 64, 32, 9, 9, 48, 3, 1, False),
+    ("1x1", 3, 160, 0, 7, 11, 320, 1, 1, False),
+    ("1x1_concat", 2, 128, 64, 8, 8, 64, 1, 1, False),
+    ("odd_n", 1, 32, 0, 5, 5, 4, 3, 1, False),
+    ("unet_l0", 1, 320, 0, 64, 64, 320, 3, 1, False),
+]
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("case", CONV_CASES, ids=[c[0] for c in CONV_CASES])
+def test_conv2d(case, dt):
+    name, B, c0, c1, H, W, Co, k, s, up = case
+    torch.manual_seed(0)
+    x = torch.randn(B, c0 + c1, H, W)
+    w = torch.randn(Co, c0 + c1, k, k) / (k * (c0 + c1) ** 0.5)
+    b = torch.randn(Co)
+    temb = torch.randn(B, Co + 5)
+    res_needed = not up and s == 1
+    xr = F.interpolate(x, scale_factor=2.0, mode="nearest") if up else x
+    ref = F.conv2d(xr, w, b, stride=s, padding=k // 2) + temb[:, :Co, None, None]
+    ref = F.silu(ref)
+    resid = torch.randn_like(ref) if res_needed else None
+    if res_needed:
+        ref = ref + resid
+    pc = K.PackedConv(w.to(DEV), b.to(DEV), dt)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV, dt)
+    x0 = xn[..., :c0].contiguous()
+    x1 = xn[..., c0:].contiguous() if c1 else None
+    temb_d = temb.to(DEV)
+    r_d = resid.permute(0, 2, 3, 1).contiguous().to(DEV, dt) if res_needed else None
+    out = K.conv2d(pc, x0, B, H, W, x1=x1, stride=s, upsample=up, temb=temb_d, temb_stride=temb.shape[1],
+                   residual=r_d, act=K.ACT_SILU)
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < tol(dt)
+    # NCHW epilogue (conv_out): same numbers, NCHW layout, no extras
+    out2 = K.conv2d(pc, x0, B, H, W, x1=x1, stride=s, upsample=up, out_layout=K.OUT_NCHW)
+    ref2 = F.conv2d(xr, w, b, stride=s, padding=k // 2)
+    assert rel_err(out2, ref2) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("M,Kd,N", [(8, 320, 1280), (1, 1280, 20160), (4096, 320, 2560), (333, 640, 5120)])
+def test_linear_and_geglu(M, Kd, N, dt):
+    torch.manual_seed(1)
+    x = torch.randn(M, Kd)
+    lin = torch.nn.Linear(Kd, N)
+    pc = K.PackedConv(lin.weight.to(DEV), lin.bias.to(DEV), dt)
+    y = K.linear(pc, x.to(DEV, dt), out_dtype=torch.float32)
+    with torch.no_grad():
+        ref = lin(x)
+    assert rel_err(y, ref) < tol(dt)
+    pg = K.PackedConv(lin.weight.to(DEV), lin.bias.to(DEV), dt, geglu=True)
+    g = K.linear(pg, x.to(DEV, dt), out_layout=K.OUT_GEGLU)
+    h, gate = ref.chunk(2, dim=-1)
+    assert rel_err(g, h * F.gelu(gate)) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_conv_transpose_shuffle(dt):
+    torch.manual_seed(2)
+    ct = torch.nn.ConvTranspose2d(64, 32, 2, stride=2)
+    x = torch.randn(2, 64, 7, 9)
+    pc = K.PackedConv(ct.weight.to(DEV), ct.bias.to(DEV), dt, shuffle2=True)
+    y = K.conv2d(pc, x.permute(0, 2, 3, 1).contiguous().to(DEV, dt), 2, 7, 9, out_layout=K.OUT_SHUFFLE2)
+    with torch.no_grad():
+        ref = ct(x)
+    assert rel_err(y.permute(0, 3, 1, 2), ref) < tol(dt)
+
+
+# ------------------------------------------------------------------------------ attention
+def _attn_ref(q, k, v, heads):
+    B, N, C = q.shape
+    d = C // heads
+    sp = lambda t: t.reshape(B, t.shape[1], heads, d).permute(0, 2, 1, 3)  # noqa: E731
+    o = torch.softmax(sp(q) @ sp(k).transpose(-1, -2) * d ** -0.5, -1) @ sp(v)
+    return o.permute(0, 2, 1, 3).reshape(B, N, C)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("B,N,L,C", [(2, 4096, 4096, 320), (2, 1024, 1024, 640), (2, 256, 256, 1280),
+                                     (3, 64, 64, 1280), (2, 200, 77, 320), (1, 100, 130, 640)])
+def test_attention(B, N, L, C, dt):
+    torch.manual_seed(3)
+    q, k, v = torch.randn(B, N, C), torch.randn(B, L, C), torch.randn(B, L, C)
+    ref = _attn_ref(q, k, v, 8)
+    if N == L:   # the UNet layout: q|k|v packed in one [B, N, 3C] buffer
+        qkv = torch.cat([q, k, v], -1).to(DEV, dt)
+        o = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, 8, C // 8, N, N, 3 * C, 3 * C, 3 * C)
+    else:        # cross-attention layout
+        kv = torch.cat([k, v], -1).to(DEV, dt)
+        o = K.attention(q.to(DEV, dt), kv, kv[..., C:], B, 8, C // 8, N, L, C, 2 * C, 2 * C)
+    assert rel_err(o, ref) < tol(dt)
+
+
+def test_attention_softmax_spike():
+    """Force the online-softmax rescale: a huge logit in the LAST kv tile of some rows."""
+    torch.manual_seed(4)
+    B, N, C = 1, 512, 320
+    q, k, v = torch.randn(B, N, C), torch.randn(B, N, C), torch.randn(B, N, C)
+    k[0, 500] = q[0, 7] * 4.0
+    k[0, 3] = -q[0, 9] * 4.0
+    ref = _attn_ref(q, k, v, 8)
+    qkv = torch.cat([q, k, v], -1).to(DEV)
+    o = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, 8, 40, N, N, 3 * C, 3 * C, 3 * C)
+    assert rel_err(o, ref) < 1e-4
+
+
+# ------------------------------------------------------------------------------ norms
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("B,HW,c0,c1,G,eps,act", [(2, 4096, 320, 0, 32, 1e-5, True), (2, 256, 1280, 1280, 32, 1e-5, True),
+                                                  (3, 100, 640, 320, 32, 1e-6, False), (1, 64, 64, 0, 16, 1e-6, True)])
+def test_group_norm(B, HW, c0, c1, G, eps, act, dt):
+    torch.manual_seed(5)
+    x = torch.randn(B, HW, c0 + c1) * 3 + 1.5
+    gam, bet = torch.randn(c0 + c1), torch.randn(c0 + c1)
+    ref = F.group_norm(x.permute(0, 2, 1), G, gam, bet, eps).permute(0, 2, 1)
+    if act:
+        ref = F.silu(ref)
+    xd = x.to(DEV, dt)
+    y = K.group_norm(xd[..., :c0].contiguous(), B, HW, G, gam.to(DEV), bet.to(DEV), eps,
+                     K.ACT_SILU if act else K.ACT_NONE, x1=xd[..., c0:].contiguous() if c1 else None)
+    assert rel_err(y, ref) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("rows,C,eps,act", [(4096, 320, 1e-5, False), (333, 1280, 1e-5, False),
+                                            (1000, 256, 1e-6, True), (17, 2560, 1e-5, False)])
+def test_layer_norm(rows, C, eps, act, dt):
+    torch.manual_seed(6)
+    x = torch.randn(rows, C) * 2 - 0.5
+    gam, bet = torch.randn(C), torch.randn(C)
+    ref = F.layer_norm(x, (C,), gam, bet, eps)
+    if act:
+        ref = F.silu(ref)
+    y = K.layer_norm(x.to(DEV, dt), gam.to(DEV), bet.to(DEV), eps, K.ACT_SILU if act else K.ACT_NONE)
+    assert rel_err(y, ref) < tol(dt)
+
+
+# ------------------------------------------------------------------------------ timestep / DDIM
+def test_timestep_proj():
+    import math
+    t = torch.tensor([999.0, 0.0, 421.0, 19.0])
+    half = 160
+    freqs = torch.exp(-math.log(10000) * torch.arange(half, dtype=torch.float32) / half)
+    emb = t[:, None] * freqs[None]
+    ref = torch.cat([torch.cos(emb), torch.sin(emb)], -1)
+    y = K.timestep_proj(t.to(DEV), 4, freqs.to(DEV), 320, True, torch.float32)
+    assert (y.cpu() - ref).abs().max().item() < 2e-5
+    y1 = K.timestep_proj(t[:1].to(DEV), 4, freqs.to(DEV), 320, False, torch.float32)
+    ref1 = torch.cat([torch.sin(emb[:1]), torch.cos(emb[:1])], -1).expand(4, -1)
+    assert (y1.cpu() - ref1).abs().max().item() < 2e-5
+
+
+@pytest.mark.parametrize("cname", list(DDIM_CONFIGS))
+def test_ddim_against_reference_golden(cname):
+    from ldmseg.schedulers import DDIMNoiseScheduler
+    z = load("ddim.npz")
+    s = DDIMNoiseScheduler(**DDIM_CONFIGS[cname], device=DEV, verbose=False)
+    s.set_timesteps_inference(50)
+    mo = torch.from_numpy(z[f"{cname}__step_model_output"]).to(DEV)
+    x = torch.from_numpy(z[f"{cname}__step_sample"]).to(DEV)
+    for t in z[f"{cname}__step_t"]:
+        for clipped in (0, 1):
+            for tt in (int(t), torch.tensor(int(t), device=DEV)):      # host int and device scalar
+                r = s.step(mo, tt, x, use_clipped_model_output=bool(clipped))
+                np.testing.assert_allclose(r.prev_sample.cpu().numpy(), z[f"{cname}__step_{t}_{clipped}__prev"],
+                                           rtol=1e-5, atol=1e-6)
+                np.testing.assert_allclose(r.pred_original_sample.cpu().numpy(),
+                                           z[f"{cname}__step_{t}_{clipped}__x0"], rtol=1e-5, atol=1e-6)
+    tb = torch.from_numpy(z[f"{cname}__an_t"]).to(DEV)
+    x0 = torch.from_numpy(z[f"{cname}__an_x0"]).to(DEV)
+    eps = torch.from_numpy(z[f"{cname}__an_eps"]).to(DEV)
+    np.testing.assert_allclose(s.add_noise(x0, eps.clone(), tb).cpu().numpy(), z[f"{cname}__an_out"], rtol=1e-5,
+                               atol=1e-6)
+    np.testing.assert_allclose(s.add_noise(x0, eps.clone(), tb, scale=2.0).cpu().numpy(), z[f"{cname}__an_out_s2"],
+                               rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(s.remove_noise(x, eps, tb).cpu().numpy(), z[f"{cname}__rn_out"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(s.remove_noise(x, eps, tb, 0.5).cpu().numpy(), z[f"{cname}__rn_out_s2"], rtol=1e-5,
+                               atol=1e-5)
+
+
+# ------------------------------------------------------------------------------ bit codec (bit-exact)
+def test_bit_codec_known_answer_pngs():
+    from ldmseg.data import decode_bitmap, encode_bitmap
+    z = load("codec.npz")
+    sem = torch.from_numpy(z["fixture_semseg"].astype(np.int64)).to(DEV)
+    planes, _ = encode_bitmap(sem, n=16, fill_value=0.5, ignore_label=0)
+    assert np.array_equal((planes.cpu().numpy() * 255).astype(np.uint8), z["fixture_bits_u8"])
+    assert np.array_equal(decode_bitmap(2 * planes - 1).cpu().numpy(), z["fixture_decode"])
+
+
+@pytest.mark.parametrize("case", list(load("codec.npz")["cases"]))
+def test_bit_codec_cases(case):
+    from ldmseg.data import decode_bitmap, encode_bitmap
+    z = load("codec.npz")
+    i = list(z["cases"]).index(case)
+    n, ign = int(z["cases_n"][i]), int(z["cases_ignore"][i])
+    ids = torch.from_numpy(z[f"{case}__ids"]).to(DEV)
+    planes, mask = encode_bitmap(ids, n=n, fill_value=0.5, ignore_label=ign)
+    assert np.array_equal(planes.cpu().numpy(), z[f"{case}__enc"])
+    assert np.array_equal(mask.cpu().numpy(), z[f"{case}__ignore_mask"])
+    assert np.array_equal(decode_bitmap(2 * planes - 1).cpu().numpy(), z[f"{case}__dec_clean"])
+    noisy = torch.from_numpy(z[f"{case}__noisy"]).to(DEV)
+    assert np.array_equal(decode_bitmap(noisy).cpu().numpy(), z[f"{case}__dec_noisy"])
+
+
+def test_bit_codec_batched_roundtrip_full_size():
+    """Size-independent property at the KITTI frame size: decode(2*encode-1) == ids (31 -> 0)."""
+    from ldmseg.data import decode_bitmap, encode_bitmap
+    g = torch.Generator(device=DEV).manual_seed(0)
+    ids = torch.randint(0, 32, (8, 192, 640), generator=g, device=DEV)
+    planes, mask = encode_bitmap(ids, n=5, fill_value=0.5, ignore_label=255)
+    assert planes.shape == (8, 5, 192, 640) and not mask.any()
+    dec = decode_bitmap(2 * planes - 1)
+    exp = ids.clone()
+    exp[exp == 31] = 0
+    assert torch.equal(dec, exp)
+
+
+# ------------------------------------------------------------------------------ resize / layout
+@pytest.mark.parametrize("size,sf", [((64, 64), None), (None, 2), ((192, 640), None), (None, 4)])
+def test_resize_bilinear(size, sf):
+    torch.manual_seed(7)
+    x = torch.randn(2, 5, 24, 80)
+    ref = F.interpolate(x, size=size, scale_factor=sf, mode="bilinear", align_corners=False)
+    y = K.resize_bilinear(x.to(DEV), size=size, scale_factor=sf)
+    assert rel_err(y, ref) < 1e-5
+    y2 = K.resize_bilinear(x.to(DEV), size=size, scale_factor=sf, mul=2.0, add=-1.0)
+    assert rel_err(y2, 2 * ref - 1) < 1e-5
+
+
+def test_nchw_to_nhwc_concat():
+    a, b, c = torch.randn(2, 4, 8, 8), torch.randn(2, 4, 8, 8), torch.randn(2, 4, 8, 8)
+    y = K.nchw_to_nhwc([a.to(DEV), b.to(DEV, torch.bfloat16), c.to(DEV)], 16, torch.float32)
+    ref = torch.cat([a, b.bfloat16().float(), c, torch.zeros(2, 4, 8, 8)], 1).permute(0, 2, 3, 1)
+    assert torch.equal(y.cpu(), ref)

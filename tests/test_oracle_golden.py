@@ -1,0 +1,97 @@
+"""Pin the CPU oracle (oracle/) against the reference's golden vectors (tests/golden/)."""
+import numpy as np
+import pytest
+import torch
+
+from golden_utils import DDIM_CONFIGS, VAE_CONFIGS, load, vae_state_dict
+from oracle import codec, ddim, dvpq, vae
+
+
+# ----------------------------------------------------------------------------- codec
+def test_codec_known_answer_pngs():
+    z = load("codec.npz")
+    planes, _ = codec.encode_bitmap(z["fixture_semseg"].astype(np.int64), n=16, ignore_label=0)
+    assert np.array_equal((planes * 255).astype(np.uint8), z["fixture_bits_u8"])
+    dec = codec.decode_bitmap(2 * planes - 1)
+    assert np.array_equal(dec, z["fixture_decode"])
+
+
+@pytest.mark.parametrize("case", list(load("codec.npz")["cases"]))
+def test_codec_cases(case):
+    z = load("codec.npz")
+    i = list(z["cases"]).index(case)
+    n, ign = int(z["cases_n"][i]), int(z["cases_ignore"][i])
+    planes, mask = codec.encode_bitmap(z[f"{case}__ids"], n=n, ignore_label=ign)
+    assert planes.dtype == np.float32
+    assert np.array_equal(planes, z[f"{case}__enc"])
+    assert np.array_equal(mask, z[f"{case}__ignore_mask"])
+    assert np.array_equal(codec.decode_bitmap(2 * planes - 1), z[f"{case}__dec_clean"])
+    assert np.array_equal(codec.decode_bitmap(z[f"{case}__noisy"]), z[f"{case}__dec_noisy"])
+
+
+# ----------------------------------------------------------------------------- ddim
+@pytest.mark.parametrize("cname", list(DDIM_CONFIGS))
+def test_ddim_tables_and_steps(cname):
+    z = load("ddim.npz")
+    kw = DDIM_CONFIGS[cname]
+    betas, ac, final = ddim.tables(kw.get("beta_schedule", "linear"), kw.get("num_train_timesteps", 1000),
+                                   kw.get("beta_start", 0.0001), kw.get("beta_end", 0.02),
+                                   kw.get("set_alpha_to_one", True))
+    np.testing.assert_array_equal(betas.numpy(), z[f"{cname}__betas"])
+    np.testing.assert_array_equal(ac.numpy(), z[f"{cname}__alphas_cumprod"])
+    assert float(final) == float(z[f"{cname}__final_alpha_cumprod"])
+    w = ddim.loss_weights(ac, kw.get("weight", "none"), kw.get("max_snr", 5.0))
+    np.testing.assert_array_equal(w.numpy(), z[f"{cname}__weights"])
+    for n in (50, 25, 7):
+        np.testing.assert_array_equal(ddim.inference_timesteps(1000, n), z[f"{cname}__timesteps_{n}"])
+    np.testing.assert_array_equal(ddim.inference_timesteps(1000, 50, 300), z[f"{cname}__timesteps_50_tmin300"])
+    mo = torch.from_numpy(z[f"{cname}__step_model_output"])
+    x = torch.from_numpy(z[f"{cname}__step_sample"])
+    for t in z[f"{cname}__step_t"]:
+        for clipped in (0, 1):
+            prev, x0 = ddim.step(ac, final, 1000, 50, mo, int(t), x, kw.get("prediction_type", "epsilon"),
+                                 kw.get("clip_sample", True), kw.get("clip_sample_range", 1.0), bool(clipped))
+            np.testing.assert_allclose(prev.numpy(), z[f"{cname}__step_{t}_{clipped}__prev"], rtol=1e-6, atol=1e-6)
+            np.testing.assert_allclose(x0.numpy(), z[f"{cname}__step_{t}_{clipped}__x0"], rtol=1e-6, atol=1e-6)
+    tb = torch.from_numpy(z[f"{cname}__an_t"])
+    x0 = torch.from_numpy(z[f"{cname}__an_x0"])
+    eps = torch.from_numpy(z[f"{cname}__an_eps"])
+    np.testing.assert_allclose(ddim.add_noise(ac, x0, eps, tb).numpy(), z[f"{cname}__an_out"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(ddim.add_noise(ac, x0, eps, tb, 2.0).numpy(), z[f"{cname}__an_out_s2"],
+                               rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(ddim.remove_noise(ac, x, eps, tb).numpy(), z[f"{cname}__rn_out"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(ddim.remove_noise(ac, x, eps, tb, 0.5).numpy(), z[f"{cname}__rn_out_s2"],
+                               rtol=1e-6, atol=1e-6)
+
+
+# ----------------------------------------------------------------------------- vae
+@pytest.mark.parametrize("cname", list(VAE_CONFIGS))
+def test_vae_encode_decode(cname):
+    torch.set_num_threads(8)
+    z = load("vae.npz")
+    cfg = VAE_CONFIGS[cname]
+    sd = vae_state_dict(z, cname)
+    assert sorted(sd) == sorted(z[f"{cname}__keys"])
+    x = torch.from_numpy(z[f"{cname}__x"])
+    with torch.no_grad():
+        moments, mean, logvar, std = vae.encode(sd, x, cfg)
+        np.testing.assert_allclose(moments.numpy(), z[f"{cname}__moments"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(mean.numpy(), z[f"{cname}__mean"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(logvar.numpy(), z[f"{cname}__logvar"], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(std.numpy(), z[f"{cname}__std"], rtol=1e-5, atol=1e-5)
+        dec_n = vae.decode(sd, mean, cfg, interpolate=False)
+        dec_i = vae.decode(sd, mean, cfg, interpolate=True)
+    np.testing.assert_allclose(dec_n.numpy(), z[f"{cname}__dec_nointerp"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(dec_i.numpy(), z[f"{cname}__dec_interp"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(dec_n.numpy(), z[f"{cname}__forward"], rtol=1e-5, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- dvpq
+def test_vpq_eval():
+    z = load("vpq.npz")
+    for c in range(int(z["n_cases"])):
+        iou, tp, fn, fp = dvpq.vpq_eval(z[f"c{c}__pred"], z[f"c{c}__gt"])
+        np.testing.assert_allclose(iou, z[f"c{c}__iou"], rtol=1e-12)
+        np.testing.assert_array_equal(tp, z[f"c{c}__tp"])
+        np.testing.assert_array_equal(fn, z[f"c{c}__fn"])
+        np.testing.assert_array_equal(fp, z[f"c{c}__fp"])

@@ -1,0 +1,98 @@
+// Shared device helpers for the ldmseg HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ldmseg_hip.h"
+
+typedef unsigned short bf16_t;  // storage type; arithmetic always in fp32
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) short short4_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+
+__device__ __forceinline__ float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+// round-to-nearest-even via v_cvt_pk_bf16_f32 (keeps NaN a NaN)
+__device__ __forceinline__ bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
+
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static __device__ __forceinline__ float load(const float* p) { return *p; }
+  static __device__ __forceinline__ void store(float* p, float v) { *p = v; }
+  static constexpr int kSize = 4;
+};
+template <> struct Elem<bf16_t> {
+  static __device__ __forceinline__ float load(const bf16_t* p) { return bf2f(*p); }
+  static __device__ __forceinline__ void store(bf16_t* p, float v) { *p = f2bf(v); }
+  static constexpr int kSize = 2;
+};
+
+template <typename T> __device__ __forceinline__ float to_f(T v);
+template <> __device__ __forceinline__ float to_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ float to_f<bf16_t>(bf16_t v) { return bf2f(v); }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return f2bf(v); }
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float gelu_f(float x) {  // exact (erf) GELU, torch approximate='none'
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// MFMA tiles with one code path for bf16 and exact fp32.
+//
+// mma_k32: D[16x16] += A[16 x 32] * B[32 x 16].  Lane l (g = l>>4) supplies the 8 K-values
+//   k = 8g + j (j = 0..7) of A row (l&15) and of B column (l&15).  bf16: one
+//   v_mfma_f32_16x16x32_bf16.  fp32: eight v_mfma_f32_16x16x4_f32, step j feeding k-slot g
+//   with element j — i.e. the same set of products summed in a different (exact fp32) order.
+// mma_k16: same with 4 K-values per lane (k = 4g + j); bf16 v_mfma_f32_16x16x16_bf16.
+// C/D layout (both): row = 4g + r (register r), col = l & 15.
+// ---------------------------------------------------------------------------------------
+template <typename T> struct Frag8;
+template <> struct Frag8<bf16_t> { uint4 v; };
+template <> struct Frag8<float> { uint4 v[2]; };
+template <typename T> struct Frag4;
+template <> struct Frag4<bf16_t> { uint2 v; };
+template <> struct Frag4<float> { uint4 v; };
+
+__device__ __forceinline__ void mma_k32(f32x4_t& acc, const Frag8<bf16_t>& a, const Frag8<bf16_t>& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a.v),
+                                                __builtin_bit_cast(bf16x8_t, b.v), acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mma_k32(f32x4_t& acc, const Frag8<float>& a, const Frag8<float>& b) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float* pa = reinterpret_cast<const float*>(&a.v[h]);
+    const float* pb = reinterpret_cast<const float*>(&b.v[h]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[j], pb[j], acc, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void mma_k16(f32x4_t& acc, const Frag4<bf16_t>& a, const Frag4<bf16_t>& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(short4_t, a.v),
+                                                  __builtin_bit_cast(short4_t, b.v), acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mma_k16(f32x4_t& acc, const Frag4<float>& a, const Frag4<float>& b) {
+  const float* pa = reinterpret_cast<const float*>(&a.v);
+  const float* pb = reinterpret_cast<const float*>(&b.v);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[j], pb[j], acc, 0, 0, 0);
+}
+
+#define LDM_CHECK_LAUNCH()                                   \
+  do {                                                       \
+    hipError_t _e = hipGetLastError();                       \
+    if (_e != hipSuccess) return LDM_ERR_LAUNCH;             \
+  } while (0)

@@ -1,0 +1,320 @@
+// Elementwise / boundary kernels of the denoising path: timestep projection, fused DDIM
+// step / add_noise / remove_noise, bit-channel mask codec, NCHW->NHWC input gather,
+// bilinear resize and the seg-VAE gaussian posterior.  All HBM-bound; one thread per
+// element (or per pixel), grid-stride, no host synchronisation (graph-capturable).
+#include "common.h"
+
+namespace {
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+inline unsigned grid_for(int64_t n, int64_t cap = 256 * 32) {
+  int64_t b = (n + 255) / 256;
+  if (b < 1) b = 1;
+  return (unsigned)std::min<int64_t>(b, cap);
+}
+
+template <typename T>
+__device__ __forceinline__ float ld(const void* p, int64_t i) {
+  return to_f(reinterpret_cast<const T*>(p)[i]);
+}
+__device__ __forceinline__ float ld_dt(const void* p, int64_t i, int dt) {
+  return dt == LDM_BF16 ? ld<bf16_t>(p, i) : ld<float>(p, i);
+}
+__device__ __forceinline__ void st_dt(void* p, int64_t i, float v, int dt) {
+  if (dt == LDM_BF16) reinterpret_cast<bf16_t*>(p)[i] = f2bf(v);
+  else reinterpret_cast<float*>(p)[i] = v;
+}
+// torch semantics: a fp32 table cast to the sample dtype before use (ddim_scheduler.py:168,202)
+__device__ __forceinline__ float table_in_dtype(float a, int dt) { return dt == LDM_BF16 ? bf2f(f2bf(a)) : a; }
+
+// ------------------------------------------------------------------ timestep projection
+__global__ void tproj_kernel(const float* __restrict__ t, int n_t, int batch, const float* __restrict__ freqs,
+                             int dim, int flip, void* out, int dtype) {
+  const int half = dim / 2;
+  const int64_t total = (int64_t)batch * dim;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int b = (int)(i / dim), j = (int)(i - (int64_t)b * dim);
+    const float tv = t[n_t == 1 ? 0 : b];
+    const int f = j < half ? j : j - half;
+    const float arg = tv * freqs[f];
+    const bool first = j < half;
+    // layout [sin || cos], flipped to [cos || sin] when flip_sin_to_cos
+    const bool use_cos = flip ? first : !first;
+    st_dt(out, i, use_cos ? cosf(arg) : sinf(arg), dtype);
+  }
+}
+
+// ------------------------------------------------------------------ DDIM
+struct DdimArgs {
+  const void* mo; int mo_dt;
+  const void* x; int x_dt;
+  void* prev; void* x0; int out_dt;
+  int64_t n;
+  const int64_t* t;
+  const float* ac;
+  float final_ac;
+  int step_ratio, pred, clip;
+  float clip_range;
+  int use_clipped;
+  int ntrain;
+};
+
+__device__ __forceinline__ float table_at(const float* ac, int64_t t, int ntrain) {
+  return (t >= 0 && t < ntrain) ? ac[t] : __int_as_float(0x7fc00000);  // NaN, never an OOB read
+}
+
+__global__ void ddim_step_kernel(const DdimArgs a) {
+  const int64_t t = *a.t;
+  const int64_t pt = t - a.step_ratio;
+  const float at = table_at(a.ac, t, a.ntrain);
+  const float ap = pt >= 0 ? table_at(a.ac, pt, a.ntrain) : a.final_ac;
+  const float bt = 1.0f - at;
+  const float sa = sqrtf(at), sb = sqrtf(bt);
+  const float sap = sqrtf(ap), sbp = sqrtf(1.0f - ap);
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * 256) {
+    const float m = ld_dt(a.mo, i, a.mo_dt);
+    const float x = ld_dt(a.x, i, a.x_dt);
+    float x0, eps;
+    if (a.pred == LDM_PRED_EPSILON) { x0 = (x - sb * m) / sa; eps = m; }
+    else if (a.pred == LDM_PRED_SAMPLE) { x0 = m; eps = (x - sa * x0) / sb; }
+    else { x0 = sa * x - sb * m; eps = sa * m + sb * x; }
+    if (a.clip) x0 = fminf(fmaxf(x0, -a.clip_range), a.clip_range);
+    if (a.use_clipped) eps = (x - sa * x0) / sb;
+    const float prev = sap * x0 + sbp * eps;
+    if (a.prev) st_dt(a.prev, i, prev, a.out_dt);
+    if (a.x0) st_dt(a.x0, i, x0, a.out_dt);
+  }
+}
+
+__global__ void add_noise_kernel(const void* x0, const void* noise, const int64_t* t, const float* ac, int ntrain,
+                                 float scale, int64_t per, int64_t n, void* out, int dt) {
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / per;
+    const float a = table_in_dtype(table_at(ac, t[b], ntrain), dt);
+    const float c0 = sqrtf(a) * scale, c1 = sqrtf(1.0f - a);
+    st_dt(out, i, c0 * ld_dt(x0, i, dt) + c1 * ld_dt(noise, i, dt), dt);
+  }
+}
+
+__global__ void remove_noise_kernel(const void* xt, const void* noise, const int64_t* t, const float* ac,
+                                    int ntrain, float scale, int64_t per, int64_t n, void* out, int dt) {
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / per;
+    const float a = table_in_dtype(table_at(ac, t[b], ntrain), dt);
+    st_dt(out, i, (ld_dt(xt, i, dt) - sqrtf(1.0f - a) * ld_dt(noise, i, dt)) / (sqrtf(a) * scale), dt);
+  }
+}
+
+// ------------------------------------------------------------------ bit codec
+__global__ void bit_encode_kernel(const int64_t* __restrict__ ids, int batch, int64_t hw, int n, int64_t ignore,
+                                  float fill, float* __restrict__ planes, uint8_t* __restrict__ mask) {
+  const int64_t total = (int64_t)batch * hw;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / hw, pix = i - b * hw;
+    const int64_t id = ids[i];
+    const bool ign = id == ignore;
+    if (mask) mask[i] = ign ? 1 : 0;
+    float* pl = planes + b * n * hw + pix;
+    for (int j = 0; j < n; ++j) pl[(int64_t)j * hw] = ign ? fill : (float)((id >> j) & 1);
+  }
+}
+
+template <typename T>
+__global__ void bit_decode_kernel(const T* __restrict__ planes, int batch, int n, int64_t hw, int drop31,
+                                  int64_t* __restrict__ ids) {
+  const int64_t total = (int64_t)batch * hw;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / hw, pix = i - b * hw;
+    const T* pl = planes + b * n * hw + pix;
+    int64_t v = 0;
+    for (int j = 0; j < n; ++j) v |= (int64_t)(to_f(pl[(int64_t)j * hw]) > 0.f) << j;
+    if (drop31 && v == 31) v = 0;
+    ids[i] = v;
+  }
+}
+
+// ------------------------------------------------------------------ NCHW sources -> NHWC
+__global__ void nchw_to_nhwc_kernel(const void* s0, int c0, int d0, const void* s1, int c1, int d1, const void* s2,
+                                    int c2, int d2, int batch, int hw, int cpad, void* out, int dt) {
+  const int64_t total = (int64_t)batch * hw;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / hw, pix = i - b * hw;
+    int c = 0;
+    for (int k = 0; k < c0; ++k, ++c) st_dt(out, i * cpad + c, ld_dt(s0, (b * c0 + k) * hw + pix, d0), dt);
+    for (int k = 0; k < c1; ++k, ++c) st_dt(out, i * cpad + c, ld_dt(s1, (b * c1 + k) * hw + pix, d1), dt);
+    for (int k = 0; k < c2; ++k, ++c) st_dt(out, i * cpad + c, ld_dt(s2, (b * c2 + k) * hw + pix, d2), dt);
+    for (; c < cpad; ++c) st_dt(out, i * cpad + c, 0.f, dt);
+  }
+}
+
+// ------------------------------------------------------------------ bilinear (align_corners=False)
+__global__ void resize_bilinear_kernel(const void* x, int64_t planes, int hi, int wi, int ho, int wo, float sh,
+                                       float sw, float mul, float add, void* out, int idt, int odt) {
+  const int64_t total = planes * ho * wo;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t pl = i / ((int64_t)ho * wo);
+    const int r = (int)(i - pl * ho * wo);
+    const int oy = r / wo, ox = r - oy * wo;
+    float fy = fmaxf((oy + 0.5f) * sh - 0.5f, 0.f);
+    float fx = fmaxf((ox + 0.5f) * sw - 0.5f, 0.f);
+    const int y0 = min((int)fy, hi - 1), x0 = min((int)fx, wi - 1);
+    const int y1 = y0 + (y0 < hi - 1 ? 1 : 0), x1 = x0 + (x0 < wi - 1 ? 1 : 0);
+    const float ly = fy - y0, lx = fx - x0;
+    const float hy = 1.f - ly, hx = 1.f - lx;
+    const int64_t base = pl * hi * wi;
+    const float v00 = ld_dt(x, base + (int64_t)y0 * wi + x0, idt), v01 = ld_dt(x, base + (int64_t)y0 * wi + x1, idt);
+    const float v10 = ld_dt(x, base + (int64_t)y1 * wi + x0, idt), v11 = ld_dt(x, base + (int64_t)y1 * wi + x1, idt);
+    const float v = hy * (hx * v00 + lx * v01) + ly * (hx * v10 + lx * v11);
+    st_dt(out, i, v * mul + add, odt);
+  }
+}
+
+// ------------------------------------------------------------------ gaussian posterior (NCHW moments)
+__global__ void posterior_kernel(const void* mom, int batch, int hw, int L, int clampo, int act, float* mean,
+                                 float* logvar, float* stdv, float* var, int dt) {
+  const int64_t total = (int64_t)batch * L * hw;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t b = i / ((int64_t)L * hw);
+    const int64_t r = i - b * L * hw;  // (l, pix)
+    float mu = ld_dt(mom, b * 2 * L * hw + r, dt);
+    float lv = ld_dt(mom, b * 2 * L * hw + (int64_t)L * hw + r, dt);
+    if (clampo) { mu = fminf(fmaxf(mu, -5.f), 5.f); lv = fminf(fmaxf(lv, -5.f), 5.f); }
+    if (act == LDM_POST_TANH) mu = tanhf(mu);
+    else if (act == LDM_POST_SIGMOID) mu = 2.f / (1.f + expf(-mu)) - 1.f;
+    else if (act == LDM_POST_CLIP) mu = fminf(fmaxf(mu, -1.f), 1.f);
+    lv = fminf(fmaxf(lv, -30.f), 20.f);
+    if (mean) mean[i] = mu;
+    if (logvar) logvar[i] = lv;
+    if (stdv) stdv[i] = expf(0.5f * lv);
+    if (var) var[i] = expf(lv);
+  }
+}
+
+}  // namespace
+
+extern "C" int ldm_timestep_proj(const float* t, int n_t, int batch, const float* freqs, int dim, int flip,
+                                 void* out, int dtype, ldm_stream_t stream) {
+  if (!t || !freqs || !out || batch <= 0 || dim <= 0 || dim % 2 || (n_t != 1 && n_t != batch)) return LDM_ERR_ARG;
+  if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
+  hipLaunchKernelGGL(tproj_kernel, dim3(grid_for((int64_t)batch * dim)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), t, n_t, batch, freqs, dim, flip, out, dtype);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" int ldm_ddim_step(const ldm_ddim_step_params* p, ldm_stream_t stream) {
+  if (!p || !p->model_output || !p->sample || !p->t || !p->alphas_cumprod || p->n < 0) return LDM_ERR_ARG;
+  if (!p->prev && !p->x0) return LDM_ERR_ARG;
+  if (p->prediction_type < 0 || p->prediction_type > 2 || p->step_ratio <= 0) return LDM_ERR_ARG;
+  if (p->n == 0) return LDM_OK;
+  DdimArgs a;
+  a.mo = p->model_output; a.mo_dt = p->mo_dtype; a.x = p->sample; a.x_dt = p->x_dtype;
+  a.prev = p->prev; a.x0 = p->x0; a.out_dt = p->out_dtype; a.n = p->n; a.t = p->t; a.ac = p->alphas_cumprod;
+  a.final_ac = p->final_alpha_cumprod; a.step_ratio = p->step_ratio; a.pred = p->prediction_type;
+  a.clip = p->clip_sample; a.clip_range = p->clip_range; a.use_clipped = p->use_clipped_model_output;
+  a.ntrain = p->num_train_timesteps;
+  if (a.ntrain <= 0) return LDM_ERR_ARG;
+  hipLaunchKernelGGL(ddim_step_kernel, dim3(grid_for(p->n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" int ldm_ddim_add_noise(const void* x0, const void* noise, const int64_t* t, const float* ac, int ntrain,
+                                  float scale, int batch, int64_t per, void* out, int dtype, ldm_stream_t stream) {
+  if (!x0 || !noise || !t || !ac || !out || batch <= 0 || per < 0 || ntrain <= 0) return LDM_ERR_ARG;
+  const int64_t n = (int64_t)batch * per;
+  if (n == 0) return LDM_OK;
+  hipLaunchKernelGGL(add_noise_kernel, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), x0,
+                     noise, t, ac, ntrain, scale, per, n, out, dtype);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" int ldm_ddim_remove_noise(const void* xt, const void* noise, const int64_t* t, const float* ac, int ntrain,
+                                     float scale, int batch, int64_t per, void* out, int dtype, ldm_stream_t stream) {
+  if (!xt || !noise || !t || !ac || !out || batch <= 0 || per < 0 || ntrain <= 0) return LDM_ERR_ARG;
+  const int64_t n = (int64_t)batch * per;
+  if (n == 0) return LDM_OK;
+  hipLaunchKernelGGL(remove_noise_kernel, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), xt,
+                     noise, t, ac, ntrain, scale, per, n, out, dtype);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" int ldm_bit_encode(const int64_t* ids, int batch, int64_t hw, int n, int64_t ignore_label,
+                              float fill_value, float* planes, uint8_t* ignore_mask, ldm_stream_t stream) {
+  if (batch < 0 || hw < 0 || n <= 0 || n > 62) return LDM_ERR_ARG;
+  const int64_t total = (int64_t)batch * hw;
+  if (total == 0) return LDM_OK;
+  if (!ids || !planes) return LDM_ERR_ARG;
+  hipLaunchKernelGGL(bit_encode_kernel, dim3(grid_for(total)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     ids, batch, hw, n, ignore_label, fill_value, planes, ignore_mask);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" int ldm_bit_decode(const void* planes, int batch, int n, int64_t hw, int drop_31, int64_t* ids, int dtype,
+                              ldm_stream_t stream) {
+  if (batch < 0 || hw < 0 || n <= 0 || n > 62) return LDM_ERR_ARG;
+  const int64_t total = (int64_t)batch * hw;
+  if (total == 0) return LDM_OK;
+  if (!planes || !ids) return LDM_ERR_ARG;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == LDM_BF16)
+    hipLaunchKernelGGL((bit_decode_kernel<bf16_t>), dim3(grid_for(total)), dim3(256), 0, s,
+                       (const bf16_t*)planes, batch, n, hw, drop_31, ids);
+  else if (dtype == LDM_F32)
+    hipLaunchKernelGGL((bit_decode_kernel<float>), dim3(grid_for(total)), dim3(256), 0, s, (const float*)planes,
+                       batch, n, hw, drop_31, ids);
+  else return LDM_ERR_ARG;
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" int ldm_nchw_to_nhwc(const void* s0, int c0, int dt0, const void* s1, int c1, int dt1, const void* s2,
+                                int c2, int dt2, int batch, int hw, int c_pad, void* out, int dtype,
+                                ldm_stream_t stream) {
+  if (!s0 || !out || c0 <= 0 || c1 < 0 || c2 < 0 || batch <= 0 || hw <= 0) return LDM_ERR_ARG;
+  if ((c1 && !s1) || (c2 && !s2) || c_pad < c0 + c1 + c2) return LDM_ERR_ARG;
+  const int64_t total = (int64_t)batch * hw;
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(grid_for(total)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     s0, c0, dt0, s1, c1, dt1, s2, c2, dt2, batch, hw, c_pad, out, dtype);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" int ldm_resize_bilinear(const void* x, int planes, int h_in, int w_in, int h_out, int w_out, float scale_h,
+                                   float scale_w, float mul, float add, void* out, int in_dtype, int out_dtype,
+                                   ldm_stream_t stream) {
+  if (!x || !out || planes <= 0 || h_in <= 0 || w_in <= 0 || h_out <= 0 || w_out <= 0) return LDM_ERR_ARG;
+  const int64_t total = (int64_t)planes * h_out * w_out;
+  hipLaunchKernelGGL(resize_bilinear_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), x, (int64_t)planes, h_in, w_in, h_out, w_out, scale_h,
+                     scale_w, mul, add, out, in_dtype, out_dtype);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" int ldm_gaussian_posterior(const void* moments, int batch, int hw, int latent_channels, int clamp_output,
+                                      int act_fn, float* mean, float* logvar, float* stdv, float* var, int dtype,
+                                      ldm_stream_t stream) {
+  if (!moments || batch <= 0 || hw <= 0 || latent_channels <= 0) return LDM_ERR_ARG;
+  const int64_t total = (int64_t)batch * latent_channels * hw;
+  hipLaunchKernelGGL(posterior_kernel, dim3(grid_for(total)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     moments, batch, hw, latent_channels, clamp_output, act_fn, mean, logvar, stdv, var, dtype);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" const char* ldm_status_string(int status) {
+  switch (status) {
+    case LDM_OK: return "ok";
+    case LDM_ERR_ARG: return "invalid argument or unsupported configuration";
+    case LDM_ERR_ALIGN: return "pointer / channel alignment violates the 16-byte vector requirement";
+    case LDM_ERR_LAUNCH: return "kernel launch failed";
+    default: return "unknown status";
+  }
+}
+
+extern "C" int ldm_abi_version(void) { return 1; }

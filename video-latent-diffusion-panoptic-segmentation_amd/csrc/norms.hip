@@ -1,0 +1,242 @@
+// GroupNorm(+SiLU) and LayerNorm over NHWC rows (ldm_group_norm / ldm_layer_norm).
+//
+// GroupNorm is HBM-bound: 3 kernels, all 16-B vectorised and coalesced along channels.
+//   gn_partial : per (batch, 64-pixel chunk) per-channel fp32 (sum, sumsq)  -> workspace
+//   gn_finalize: per (batch, group) fp64 reduction of the partials         -> (mean, rstd)
+//   gn_apply   : y = silu?((x - mean) * rstd * gamma + beta)  written as one NHWC tensor
+// Inputs may be the channel concatenation of two NHWC tensors (up-block [hidden || skip]),
+// read in place.  Algorithmic traffic: 2 reads + 1 write of the tensor.
+#include "common.h"
+
+namespace {
+
+constexpr int GN_PPC = 64;  // pixels per partial chunk
+
+template <typename T>
+__global__ __launch_bounds__(256) void gn_partial(const T* __restrict__ x0, const T* __restrict__ x1,
+                                                  int c0, int c1, int hw, int chunks,
+                                                  float2* __restrict__ part) {
+  constexpr int EPC = 16 / sizeof(T);
+  const int C = c0 + c1, V = C / EPC;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int v = blockIdx.x * 64 + tx;
+  const int chunk = blockIdx.y, b = blockIdx.z;
+  float s[EPC], ss[EPC];
+#pragma unroll
+  for (int e = 0; e < EPC; ++e) { s[e] = 0.f; ss[e] = 0.f; }
+  if (v < V) {
+    const int c = v * EPC;
+    const T* src;
+    int cs, co;
+    if (c < c0) { src = x0; cs = c0; co = c; } else { src = x1; cs = c1; co = c - c0; }
+    const int p0 = chunk * GN_PPC, p1 = min(hw, p0 + GN_PPC);
+    for (int pix = p0 + ty; pix < p1; pix += 4) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(src + ((int64_t)b * hw + pix) * cs + co);
+      const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) {
+        const float f = to_f(e[k]);
+        s[k] += f;
+        ss[k] += f * f;
+      }
+    }
+  }
+  __shared__ float red[4][64][EPC][2];
+#pragma unroll
+  for (int k = 0; k < EPC; ++k) { red[ty][tx][k][0] = s[k]; red[ty][tx][k][1] = ss[k]; }
+  __syncthreads();
+  if (ty == 0 && v < V) {
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) {
+      float a = 0.f, q = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { a += red[j][tx][k][0]; q += red[j][tx][k][1]; }
+      part[((int64_t)b * chunks + chunk) * C + v * EPC + k] = make_float2(a, q);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gn_finalize(const float2* __restrict__ part, int C, int hw, int chunks,
+                                                   int groups, float eps, float2* __restrict__ stats) {
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cpg = C / groups;
+  const int n = chunks * cpg;
+  for (int gi = wave; gi < groups; gi += 4) {
+    double a = 0.0, q = 0.0;
+    for (int i = lane; i < n; i += 64) {
+      const int ch = i / cpg, cc = i - ch * cpg;
+      const float2 v = part[((int64_t)b * chunks + ch) * C + gi * cpg + cc];
+      a += v.x;
+      q += v.y;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); q += __shfl_xor(q, o, 64); }
+    if (lane == 0) {
+      const double cnt = (double)hw * cpg;
+      const double mean = a / cnt;
+      double var = q / cnt - mean * mean;
+      if (var < 0.0) var = 0.0;
+      stats[b * groups + gi] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x0, const T* __restrict__ x1, int c0, int c1,
+                                                int hw, int64_t nvec, int groups, const float2* __restrict__ stats,
+                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                int act, T* __restrict__ out) {
+  constexpr int EPC = 16 / sizeof(T);
+  const int C = c0 + c1, V = C / EPC, cpg = C / groups;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
+    const int64_t m = i / V;
+    const int v = (int)(i - m * V);
+    const int b = (int)(m / hw);
+    const int c = v * EPC;
+    const uint4 raw = (c < c0) ? *reinterpret_cast<const uint4*>(x0 + m * c0 + c)
+                               : *reinterpret_cast<const uint4*>(x1 + m * c1 + (c - c0));
+    const T* e = reinterpret_cast<const T*>(&raw);
+    uint4 res;
+    T* r = reinterpret_cast<T*>(&res);
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) {
+      const int ch = c + k;
+      const float2 st = stats[b * groups + ch / cpg];
+      float y = (to_f(e[k]) - st.x) * st.y * gamma[ch] + beta[ch];
+      if (act == LDM_ACT_SILU) y = silu_f(y);
+      r[k] = from_f<T>(y);
+    }
+    *reinterpret_cast<uint4*>(out + m * C + c) = res;
+  }
+}
+
+// LayerNorm over the last dim: one wave per row, two-pass (mean, then centred variance) in fp32.
+template <typename T, int MAXV>
+__global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, int rows, int C,
+                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                 float eps, int act, T* __restrict__ out) {
+  constexpr int EPC = 16 / sizeof(T);
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int V = C / EPC;
+  const T* xr = x + (int64_t)row * C;
+  float vals[MAXV][EPC];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int v = lane + 64 * i;
+    if (v < V) {
+      const uint4 raw = *reinterpret_cast<const uint4*>(xr + v * EPC);
+      const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) { vals[i][k] = to_f(e[k]); s += vals[i][k]; }
+    }
+  }
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    if (lane + 64 * i < V) {
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) { const float d = vals[i][k] - mean; q += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / C + eps);
+  T* orow = out + (int64_t)row * C;
+#pragma unroll
+  for (int i = 0; i < MAXV; ++i) {
+    const int v = lane + 64 * i;
+    if (v < V) {
+      uint4 res;
+      T* r = reinterpret_cast<T*>(&res);
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) {
+        const int ch = v * EPC + k;
+        float y = (vals[i][k] - mean) * rstd * gamma[ch] + beta[ch];
+        if (act == LDM_ACT_SILU) y = silu_f(y);
+        r[k] = from_f<T>(y);
+      }
+      *reinterpret_cast<uint4*>(orow + v * EPC) = res;
+    }
+  }
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+template <typename T>
+int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups, const float* gamma,
+              const float* beta, float eps, int act, void* out, void* ws, hipStream_t s) {
+  constexpr int EPC = 16 / sizeof(T);
+  const int C = c0 + c1;
+  const int V = C / EPC;
+  const int chunks = (hw + GN_PPC - 1) / GN_PPC;
+  float2* part = static_cast<float2*>(ws);
+  float2* stats = part + (size_t)batch * chunks * C;
+  hipLaunchKernelGGL((gn_partial<T>), dim3((V + 63) / 64, chunks, batch), dim3(256), 0, s,
+                     static_cast<const T*>(x0), static_cast<const T*>(x1), c0, c1, hw, chunks, part);
+  LDM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(gn_finalize, dim3(batch), dim3(256), 0, s, part, C, hw, chunks, groups, eps, stats);
+  LDM_CHECK_LAUNCH();
+  const int64_t nvec = (int64_t)batch * hw * V;
+  const int64_t blocks = std::min<int64_t>((nvec + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL((gn_apply<T>), dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const T*>(x0),
+                     static_cast<const T*>(x1), c0, c1, hw, nvec, groups, stats, gamma, beta, act,
+                     static_cast<T*>(out));
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+}  // namespace
+
+extern "C" size_t ldm_group_norm_workspace_bytes(int batch, int hw, int channels) {
+  const size_t chunks = (hw + GN_PPC - 1) / GN_PPC;
+  return (size_t)batch * chunks * channels * sizeof(float2) + (size_t)batch * 512 * sizeof(float2) + 256;
+}
+
+extern "C" int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
+                              const float* gamma, const float* beta, float eps, int act, void* out, void* workspace,
+                              int dtype, ldm_stream_t stream) {
+  if (!x0 || !out || !workspace || !gamma || !beta) return LDM_ERR_ARG;
+  if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
+  if (batch <= 0 || hw <= 0 || c0 <= 0 || c1 < 0 || (c1 > 0 && !x1) || groups <= 0 || groups > 512) return LDM_ERR_ARG;
+  const int C = c0 + c1;
+  if (C % groups) return LDM_ERR_ARG;
+  const int epc = dtype == LDM_F32 ? 4 : 8;
+  if (c0 % epc || c1 % epc) return LDM_ERR_ALIGN;
+  if (!aligned16(x0) || (x1 && !aligned16(x1)) || !aligned16(out) || !aligned16(workspace)) return LDM_ERR_ALIGN;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == LDM_BF16)
+    return gn_launch<bf16_t>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, workspace, s);
+  return gn_launch<float>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, workspace, s);
+}
+
+extern "C" int ldm_layer_norm(const void* x, int rows, int c, const float* gamma, const float* beta, float eps,
+                              int act, void* out, int dtype, ldm_stream_t stream) {
+  if (!x || !out || !gamma || !beta || rows <= 0 || c <= 0) return LDM_ERR_ARG;
+  if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
+  const int epc = dtype == LDM_F32 ? 4 : 8;
+  if (c % epc) return LDM_ERR_ALIGN;
+  if (!aligned16(x) || !aligned16(out)) return LDM_ERR_ALIGN;
+  const int V = c / epc;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid((rows + 3) / 4);
+  if (dtype == LDM_BF16) {
+    if (V <= 64 * 4) hipLaunchKernelGGL((ln_kernel<bf16_t, 4>), grid, dim3(256), 0, s, (const bf16_t*)x, rows, c,
+                                        gamma, beta, eps, act, (bf16_t*)out);
+    else if (V <= 64 * 8) hipLaunchKernelGGL((ln_kernel<bf16_t, 8>), grid, dim3(256), 0, s, (const bf16_t*)x, rows,
+                                             c, gamma, beta, eps, act, (bf16_t*)out);
+    else return LDM_ERR_ARG;
+  } else {
+    if (V <= 64 * 4) hipLaunchKernelGGL((ln_kernel<float, 4>), grid, dim3(256), 0, s, (const float*)x, rows, c,
+                                        gamma, beta, eps, act, (float*)out);
+    else if (V <= 64 * 8) hipLaunchKernelGGL((ln_kernel<float, 8>), grid, dim3(256), 0, s, (const float*)x, rows, c,
+                                             gamma, beta, eps, act, (float*)out);
+    else if (V <= 64 * 16) hipLaunchKernelGGL((ln_kernel<float, 16>), grid, dim3(256), 0, s, (const float*)x, rows,
+                                              c, gamma, beta, eps, act, (float*)out);
+    else return LDM_ERR_ARG;
+  }
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}

@@ -1,0 +1,536 @@
+"""Drop-in ``UNet`` for ldmseg/models/unet.py:24 (an SD-1.x UNet2DConditionModel subclass).
+
+The module tree and parameter names are diffusers' (so ``state_dict`` / ``load_state_dict``
+stay checkpoint-compatible, trainers_ldm_cond.py:1846-1848,1891-1894); the arithmetic of
+``forward`` (unet.py:281-436) runs entirely through the gfx950 HIP library:
+
+  NCHW sample --nchw_to_nhwc--> NHWC activations (channels contiguous) for the whole graph
+  timestep    --timestep_proj / linear(+SiLU) x2--> emb; every ResNet's time_emb_proj is
+              ONE batched GEMM whose per-(b, n) output is added in the conv1 epilogue
+  ResNet      GN+SiLU -> conv3x3 (+bias +temb) -> GN+SiLU -> conv3x3 (+bias +shortcut residual)
+              up-block skip concats are read in place by GN and the convs (never copied)
+  Transformer GN -> proj_in -> LN -> fused QKV GEMM -> flash attention -> to_out (+residual)
+              -> LN -> GEGLU GEMM (gelu epilogue) -> net.2 (+residual) -> proj_out (+residual)
+  Down/Up     stride-2 conv / conv reading the input through a nearest-2x upsample
+  out         GN+SiLU -> conv_out written straight to NCHW
+
+Only the inference forward is native this round (training backward is
+the next row); gradients do not flow through it.
+"""
+import json
+import math
+import os
+from typing import Any, Dict, Optional, Tuple, Union
+
+import torch
+import torch.nn as nn
+
+from ..ops import native as K
+from ..utils import OutputDict
+
+
+class UNetOutput(OutputDict):
+    sample: torch.FloatTensor
+
+
+# --------------------------------------------------------------------------------------
+# module tree with diffusers parameter names
+# --------------------------------------------------------------------------------------
+class Timesteps(nn.Module):
+    def __init__(self, num_channels, flip_sin_to_cos=True, downscale_freq_shift=0.0):
+        super().__init__()
+        self.num_channels = num_channels
+        self.flip_sin_to_cos = flip_sin_to_cos
+        self.downscale_freq_shift = downscale_freq_shift
+
+    def frequencies(self, device):
+        half = self.num_channels // 2
+        exponent = -math.log(10000) * torch.arange(half, dtype=torch.float32) / (half - self.downscale_freq_shift)
+        return torch.exp(exponent).to(device)
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, in_channels, time_embed_dim):
+        super().__init__()
+        self.linear_1 = nn.Linear(in_channels, time_embed_dim)
+        self.act = nn.SiLU()
+        self.linear_2 = nn.Linear(time_embed_dim, time_embed_dim)
+
+
+class ResnetBlock2D(nn.Module):
+    def __init__(self, in_channels, out_channels, temb_channels, groups=32, eps=1e-5):
+        super().__init__()
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.groups, self.eps = groups, eps
+        self.norm1 = nn.GroupNorm(groups, in_channels, eps=eps, affine=True)
+        self.conv1 = nn.Conv2d(in_channels, out_channels, 3, padding=1)
+        self.time_emb_proj = nn.Linear(temb_channels, out_channels)
+        self.norm2 = nn.GroupNorm(groups, out_channels, eps=eps, affine=True)
+        self.dropout = nn.Dropout(0.0)
+        self.conv2 = nn.Conv2d(out_channels, out_channels, 3, padding=1)
+        self.nonlinearity = nn.SiLU()
+        self.conv_shortcut = nn.Conv2d(in_channels, out_channels, 1) if in_channels != out_channels else None
+
+
+class Attention(nn.Module):
+    def __init__(self, query_dim, heads, dim_head, cross_attention_dim=None):
+        super().__init__()
+        inner = heads * dim_head
+        self.heads, self.dim_head = heads, dim_head
+        self.is_cross = cross_attention_dim is not None
+        kv_dim = cross_attention_dim or query_dim
+        self.to_q = nn.Linear(query_dim, inner, bias=False)
+        self.to_k = nn.Linear(kv_dim, inner, bias=False)
+        self.to_v = nn.Linear(kv_dim, inner, bias=False)
+        self.to_out = nn.ModuleList([nn.Linear(inner, query_dim), nn.Dropout(0.0)])
+
+
+class GEGLU(nn.Module):
+    def __init__(self, dim_in, dim_out):
+        super().__init__()
+        self.proj = nn.Linear(dim_in, dim_out * 2)
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim, mult=4):
+        super().__init__()
+        self.net = nn.ModuleList([GEGLU(dim, dim * mult), nn.Dropout(0.0), nn.Linear(dim * mult, dim)])
+
+
+class BasicTransformerBlock(nn.Module):
+    def __init__(self, dim, heads, dim_head, cross_attention_dim=None):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim)
+        self.attn1 = Attention(dim, heads, dim_head)
+        if cross_attention_dim is not None:
+            self.norm2 = nn.LayerNorm(dim)
+            self.attn2 = Attention(dim, heads, dim_head, cross_attention_dim)
+        else:
+            self.norm2 = None
+            self.attn2 = None
+        self.norm3 = nn.LayerNorm(dim)
+        self.ff = FeedForward(dim)
+
+
+class Transformer2DModel(nn.Module):
+    def __init__(self, heads, dim_head, in_channels, groups=32, cross_attention_dim=None):
+        super().__init__()
+        inner = heads * dim_head
+        self.groups = groups
+        self.norm = nn.GroupNorm(groups, in_channels, eps=1e-6, affine=True)
+        self.proj_in = nn.Conv2d(in_channels, inner, 1)
+        self.transformer_blocks = nn.ModuleList([BasicTransformerBlock(inner, heads, dim_head, cross_attention_dim)])
+        self.proj_out = nn.Conv2d(inner, in_channels, 1)
+
+
+class Downsample2D(nn.Module):
+    def __init__(self, channels):
+        super().__init__()
+        self.conv = nn.Conv2d(channels, channels, 3, stride=2, padding=1)
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, channels):
+        super().__init__()
+        self.conv = nn.Conv2d(channels, channels, 3, padding=1)
+
+
+class DownBlock(nn.Module):
+    """CrossAttnDownBlock2D (has_cross_attention) or DownBlock2D."""
+
+    def __init__(self, cin, cout, temb, layers, groups, eps, heads, attn, cross_dim, add_down):
+        super().__init__()
+        self.has_cross_attention = attn
+        self.resnets = nn.ModuleList([ResnetBlock2D(cin if i == 0 else cout, cout, temb, groups, eps)
+                                      for i in range(layers)])
+        if attn:
+            self.attentions = nn.ModuleList([Transformer2DModel(heads, cout // heads, cout, groups, cross_dim)
+                                             for _ in range(layers)])
+        self.downsamplers = nn.ModuleList([Downsample2D(cout)]) if add_down else None
+
+
+class UpBlock(nn.Module):
+    """CrossAttnUpBlock2D (has_cross_attention) or UpBlock2D."""
+
+    def __init__(self, cin, cprev, cout, temb, layers, groups, eps, heads, attn, cross_dim, add_up):
+        super().__init__()
+        self.has_cross_attention = attn
+        res = []
+        for i in range(layers):
+            skip = cin if i == layers - 1 else cout
+            rin = cprev if i == 0 else cout
+            res.append(ResnetBlock2D(rin + skip, cout, temb, groups, eps))
+        self.resnets = nn.ModuleList(res)
+        if attn:
+            self.attentions = nn.ModuleList([Transformer2DModel(heads, cout // heads, cout, groups, cross_dim)
+                                             for _ in range(layers)])
+        self.upsamplers = nn.ModuleList([Upsample2D(cout)]) if add_up else None
+
+
+class UNetMidBlock2DCrossAttn(nn.Module):
+    def __init__(self, c, temb, groups, eps, heads, cross_dim):
+        super().__init__()
+        self.has_cross_attention = True
+        self.resnets = nn.ModuleList([ResnetBlock2D(c, c, temb, groups, eps), ResnetBlock2D(c, c, temb, groups, eps)])
+        self.attentions = nn.ModuleList([Transformer2DModel(heads, c // heads, c, groups, cross_dim)])
+
+
+class _Config(dict):
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError as e:
+            raise AttributeError(k) from e
+
+
+SD_V1_CONFIG = dict(
+    sample_size=64, in_channels=4, out_channels=4, center_input_sample=False, flip_sin_to_cos=True, freq_shift=0,
+    down_block_types=("CrossAttnDownBlock2D", "CrossAttnDownBlock2D", "CrossAttnDownBlock2D", "DownBlock2D"),
+    up_block_types=("UpBlock2D", "CrossAttnUpBlock2D", "CrossAttnUpBlock2D", "CrossAttnUpBlock2D"),
+    block_out_channels=(320, 640, 1280, 1280), layers_per_block=2, downsample_padding=1, mid_block_scale_factor=1,
+    act_fn="silu", norm_num_groups=32, norm_eps=1e-5, cross_attention_dim=768, attention_head_dim=8,
+)
+
+
+# --------------------------------------------------------------------------------------
+# the drop-in UNet
+# --------------------------------------------------------------------------------------
+class UNet(nn.Module):
+    """UNet2DConditionModel-compatible module whose forward runs on the HIP kernels."""
+
+    config_name = "config.json"
+
+    def __init__(self, **kwargs):
+        super().__init__()
+        cfg = dict(SD_V1_CONFIG)
+        cfg.update({k: v for k, v in kwargs.items() if not k.startswith("_")})
+        self.config = _Config(cfg)
+        boc = list(cfg["block_out_channels"])
+        lpb = cfg["layers_per_block"]
+        G, eps = cfg["norm_num_groups"], cfg["norm_eps"]
+        heads = cfg["attention_head_dim"]
+        cross = cfg.get("cross_attention_dim")
+        temb = boc[0] * 4
+        self.conv_in = nn.Conv2d(cfg["in_channels"], boc[0], 3, padding=1)
+        self.time_proj = Timesteps(boc[0], cfg["flip_sin_to_cos"], cfg["freq_shift"])
+        self.time_embedding = TimestepEmbedding(boc[0], temb)
+        self.encoder_hid_proj = None
+        down = []
+        c = boc[0]
+        for i, bt in enumerate(cfg["down_block_types"]):
+            cin, c = c, boc[i]
+            down.append(DownBlock(cin, c, temb, lpb, G, eps, heads, "CrossAttn" in bt, cross, i < len(boc) - 1))
+        self.down_blocks = nn.ModuleList(down)
+        self.mid_block = UNetMidBlock2DCrossAttn(boc[-1], temb, G, eps, heads, cross)
+        rev = list(reversed(boc))
+        up = []
+        cprev = rev[0]
+        for i, bt in enumerate(cfg["up_block_types"]):
+            cout = rev[i]
+            cin = rev[min(i + 1, len(boc) - 1)]
+            up.append(UpBlock(cin, cprev, cout, temb, lpb + 1, G, eps, heads, "CrossAttn" in bt, cross,
+                              i < len(boc) - 1))
+            cprev = cout
+        self.up_blocks = nn.ModuleList(up)
+        self.conv_norm_out = nn.GroupNorm(G, boc[0], eps=eps)
+        self.conv_act = nn.SiLU()
+        self.conv_out = nn.Conv2d(boc[0], cfg["out_channels"], 3, padding=1)
+        self.gradient_checkpointing = False
+        self._plan = None
+        self._plan_key = None
+
+    # ------------------------------------------------------------ diffusers-style API
+    @property
+    def dtype(self) -> torch.dtype:
+        return next(self.parameters()).dtype
+
+    @property
+    def device(self) -> torch.device:
+        return next(self.parameters()).device
+
+    @classmethod
+    def from_pretrained(cls, pretrained_model_name_or_path, subfolder=None, cache_dir=None, **kwargs):
+        """Load a local diffusers UNet folder (config.json + weights), tools/main_ldm.py:147.
+
+        Only local paths are supported (no hub download); weights are read with loaders that
+        execute nothing from the file (safetensors, or torch.load(weights_only=True)).
+        """
+        path = pretrained_model_name_or_path if subfolder is None else os.path.join(pretrained_model_name_or_path,
+                                                                                    subfolder)
+        with open(os.path.join(path, cls.config_name)) as f:
+            cfg = json.load(f)
+        keep = set(SD_V1_CONFIG) | {"sample_size"}
+        model = cls(**{k: (tuple(v) if isinstance(v, list) else v) for k, v in cfg.items() if k in keep})
+        st = os.path.join(path, "diffusion_pytorch_model.safetensors")
+        if os.path.exists(st):
+            from safetensors.torch import load_file
+            sd = load_file(st)
+        else:
+            sd = torch.load(os.path.join(path, "diffusion_pytorch_model.bin"), map_location="cpu", weights_only=True)
+        sd = _remap_legacy_keys(sd)
+        model.load_state_dict(sd, strict=True)
+        return model
+
+    def enable_gradient_checkpointing(self):
+        self.gradient_checkpointing = True
+
+    def get_lr_func(self, name: str, lr_decay_rate: float = 1.0) -> float:   # unet.py:107-119
+        if name.startswith("module."):
+            name = name[len("module."):]
+        if name.startswith("conv_in.") or name.startswith("down_blocks."):
+            return lr_decay_rate
+        return 1.0
+
+    def remove_cross_attention(self):                                        # unet.py:83-105
+        blocks = list(self.down_blocks) + [self.mid_block] + list(self.up_blocks)
+        for blk in blocks:
+            if getattr(blk, "has_cross_attention", False):
+                for attn in blk.attentions:
+                    for tb in attn.transformer_blocks:
+                        tb.attn2 = None
+                        tb.norm2 = None
+        self._plan = None
+
+    def modify_encoder(self, in_channels: int = 4, init_mode_seg: str = "copy", init_mode_image: str = "copy",
+                       cond_channels: int = 0, init_mode_cond: str = "zero", separate_conv: bool = False,
+                       separate_encoder: bool = False, add_adaptor: bool = False,
+                       init_mode_adaptor: str = "random") -> None:
+        """unet.py:124-233.  The 8(+cond)-channel conv_in branch, including its quirks: the
+        'div' modes are no-ops (the quotient of ``.copy_(w) / 2.`` is discarded, :188,202) and
+        the cond 'mean' branch tests init_mode_image (:225)."""
+        assert in_channels in [4, 8], "in_channels must be 4 or 8"
+        assert separate_conv + separate_encoder <= 1
+        if separate_conv or separate_encoder:
+            raise NotImplementedError("separate_conv / separate_encoder are non-default variants, not on the "
+                                      "accelerated path (SURVEY.md §2 row 1)")
+        if in_channels != 8:
+            return
+        old = self.conv_in
+        w_old, b_old = old.weight.data, old.bias.data
+        self.new_conv = nn.Conv2d(in_channels + cond_channels, old.out_channels, kernel_size=old.kernel_size,
+                                  stride=old.stride, padding=old.padding, bias=old.bias is not None)
+        self.new_conv.to(device=w_old.device, dtype=w_old.dtype)
+        W = self.new_conv.weight.data
+        mean4 = torch.mean(w_old, dim=1, keepdim=True).repeat(1, 4, 1, 1)
+        for sl, mode, what in ((slice(0, 4), init_mode_seg, "seg"), (slice(4, 8), init_mode_image, "image")):
+            if mode in ("copy", "div"):
+                W[:, sl].copy_(w_old)
+            elif mode == "mean":
+                W[:, sl].copy_(mean4)
+            elif mode == "zero":
+                W[:, sl].zero_()
+            elif mode != "random":
+                raise NotImplementedError(f"init_mode {what} {mode} not implemented")
+        self.new_conv.bias.data.copy_(b_old)
+        assert W.shape == torch.Size([old.out_channels, 8 + cond_channels, 3, 3])
+        if cond_channels > 0:
+            if init_mode_cond == "zero":
+                W[:, 8:].zero_()
+            elif init_mode_image == "mean":
+                W[:, 8:].copy_(mean4)
+            elif init_mode_cond != "random":
+                raise NotImplementedError(f"init_mode cond {init_mode_cond} not implemented")
+        self.conv_in = self.new_conv          # aliased: state_dict holds conv_in.* AND new_conv.*
+        self._plan = None
+
+    def freeze_layers(self, layers=("norm", "time_embedding")) -> None:      # unet.py:235-279
+        for layer in layers:
+            if layer == "norm":
+                for m in self.modules():
+                    if isinstance(m, (nn.GroupNorm, nn.LayerNorm, nn.BatchNorm2d)):
+                        m.requires_grad_(False)
+            elif layer == "time_embedding":
+                self.time_embedding.requires_grad_(False)
+            elif layer in ("conv_in", "down_blocks"):
+                pass                                 # only acts with separate_encoder (not built)
+            else:
+                raise NotImplementedError(f"layer {layer} not implemented")
+
+    # ------------------------------------------------------------ packed-weight plan
+    def _signature(self):
+        return (self.dtype, self.device) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+
+    def prepare(self, force=False):
+        """(Re)pack every weight for the HIP kernels; cached until a parameter changes."""
+        key = self._signature()
+        if not force and self._plan is not None and self._plan_key == key:
+            return self._plan
+        dt = self.dtype
+        if dt not in (torch.float32, torch.bfloat16):
+            raise TypeError(f"UNet HIP path runs in float32 or bfloat16, not {dt}")
+        f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
+        P = {}
+        cin = self.conv_in.in_channels
+        cin_pad = (cin + 15) // 16 * 16
+        P["conv_in"] = K.PackedConv(self.conv_in.weight, self.conv_in.bias, dt, cin_pad=cin_pad)
+        P["cin_pad"] = cin_pad
+        P["freqs"] = self.time_proj.frequencies(self.device)
+        te = self.time_embedding
+        P["lin1"] = K.PackedConv(te.linear_1.weight, te.linear_1.bias, dt)
+        P["lin2"] = K.PackedConv(te.linear_2.weight, te.linear_2.bias, dt)
+        # all ResNets' time_emb_proj as one GEMM [sum Cout, 1280]
+        resnets = [m for m in self.modules() if isinstance(m, ResnetBlock2D)]
+        ws, bs, off = [], [], 0
+        for r in resnets:
+            ws.append(r.time_emb_proj.weight)
+            bs.append(r.time_emb_proj.bias)
+            P[id(r), "temb_off"] = off
+            off += r.out_channels
+        P["temb_proj"] = K.PackedConv(torch.cat(ws), torch.cat(bs), dt)
+        P["temb_total"] = off
+        for r in resnets:
+            P[id(r)] = dict(
+                n1=(f32(r.norm1.weight), f32(r.norm1.bias)), n2=(f32(r.norm2.weight), f32(r.norm2.bias)),
+                c1=K.PackedConv(r.conv1.weight, r.conv1.bias, dt), c2=K.PackedConv(r.conv2.weight, r.conv2.bias, dt),
+                sc=None if r.conv_shortcut is None else K.PackedConv(r.conv_shortcut.weight, r.conv_shortcut.bias, dt),
+                off=P[id(r), "temb_off"])
+        for t in [m for m in self.modules() if isinstance(m, Transformer2DModel)]:
+            tb = t.transformer_blocks[0]
+            a1 = tb.attn1
+            d = dict(norm=(f32(t.norm.weight), f32(t.norm.bias)),
+                     proj_in=K.PackedConv(t.proj_in.weight, t.proj_in.bias, dt),
+                     proj_out=K.PackedConv(t.proj_out.weight, t.proj_out.bias, dt),
+                     ln1=(f32(tb.norm1.weight), f32(tb.norm1.bias)), ln3=(f32(tb.norm3.weight), f32(tb.norm3.bias)),
+                     qkv=K.PackedConv(torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight]), None, dt),
+                     out1=K.PackedConv(a1.to_out[0].weight, a1.to_out[0].bias, dt),
+                     heads=a1.heads, dim_head=a1.dim_head,
+                     ff1=K.PackedConv(tb.ff.net[0].proj.weight, tb.ff.net[0].proj.bias, dt, geglu=True),
+                     ff2=K.PackedConv(tb.ff.net[2].weight, tb.ff.net[2].bias, dt), attn2=None)
+            if tb.attn2 is not None:
+                a2 = tb.attn2
+                d["attn2"] = dict(ln2=(f32(tb.norm2.weight), f32(tb.norm2.bias)),
+                                  q=K.PackedConv(a2.to_q.weight, None, dt),
+                                  kv=K.PackedConv(torch.cat([a2.to_k.weight, a2.to_v.weight]), None, dt),
+                                  out=K.PackedConv(a2.to_out[0].weight, a2.to_out[0].bias, dt))
+            P[id(t)] = d
+        for m in self.modules():
+            if isinstance(m, (Downsample2D, Upsample2D)):
+                P[id(m)] = K.PackedConv(m.conv.weight, m.conv.bias, dt)
+        P["out_norm"] = (f32(self.conv_norm_out.weight), f32(self.conv_norm_out.bias))
+        P["conv_out"] = K.PackedConv(self.conv_out.weight, self.conv_out.bias, dt)
+        self._plan, self._plan_key = P, key
+        return P
+
+    # ------------------------------------------------------------ HIP forward pieces
+    def _resnet(self, P, r, xs, B, H, W, temb_all):
+        p = P[id(r)]
+        x0, x1 = xs
+        h = K.group_norm(x0, B, H * W, r.groups, *p["n1"], r.eps, K.ACT_SILU, x1=x1)
+        h = K.conv2d(p["c1"], h, B, H, W, temb=temb_all[:, p["off"]:], temb_stride=temb_all.shape[1])
+        h = K.group_norm(h, B, H * W, r.groups, *p["n2"], r.eps, K.ACT_SILU)
+        if p["sc"] is not None:
+            res = K.conv2d(p["sc"], x0, B, H, W, x1=x1)
+        else:
+            assert x1 is None
+            res = x0
+        return K.conv2d(p["c2"], h, B, H, W, residual=res)
+
+    def _transformer(self, P, t, x, B, H, W, ehs):
+        p = P[id(t)]
+        C = x.shape[-1]
+        N = H * W
+        h = K.group_norm(x, B, N, t.groups, *p["norm"], 1e-6)
+        h = K.linear(p["proj_in"], h)                                    # [B, N, C]
+        n = K.layer_norm(h, *p["ln1"], 1e-5)
+        qkv = K.linear(p["qkv"], n)                                      # [B, N, 3C]
+        heads, dh = p["heads"], p["dim_head"]
+        a = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, dh, N, N, 3 * C, 3 * C, 3 * C)
+        h = K.linear(p["out1"], a, residual=h, out=h)
+        if p["attn2"] is not None and ehs is not None:
+            q2 = p["attn2"]
+            n = K.layer_norm(h, *q2["ln2"], 1e-5)
+            q = K.linear(q2["q"], n)
+            e = ehs.to(self.dtype).contiguous()
+            kv = K.linear(q2["kv"], e)                                   # [B, L, 2C]
+            L = e.shape[1]
+            a = K.attention(q, kv, kv[..., C:], B, heads, dh, N, L, C, 2 * C, 2 * C)
+            h = K.linear(q2["out"], a, residual=h, out=h)
+        n = K.layer_norm(h, *p["ln3"], 1e-5)
+        f = K.linear(p["ff1"], n, out_layout=K.OUT_GEGLU)                # [B, N, 4C]
+        h = K.linear(p["ff2"], f, residual=h, out=h)
+        return K.linear(p["proj_out"], h, residual=x)
+
+    @torch.no_grad()
+    def forward(
+        self,
+        sample: torch.FloatTensor,
+        timestep: Union[torch.Tensor, float, int],
+        encoder_hidden_states: Optional[torch.Tensor] = None,
+        class_labels: Optional[torch.Tensor] = None,
+        timestep_cond: Optional[torch.Tensor] = None,
+        attention_mask: Optional[torch.Tensor] = None,
+        cross_attention_kwargs: Optional[Dict[str, Any]] = None,
+        down_block_additional_residuals: Optional[Tuple[torch.Tensor]] = None,
+        mid_block_additional_residual: Optional[torch.Tensor] = None,
+        return_dict: bool = True,
+        timestep_img: Optional[Union[torch.Tensor, float, int]] = None,
+    ) -> Union[UNetOutput, Tuple]:
+        if class_labels is not None or timestep_cond is not None or attention_mask is not None:
+            raise NotImplementedError("class_labels / timestep_cond / attention_mask are not on the reference path")
+        if down_block_additional_residuals is not None or mid_block_additional_residual is not None:
+            raise NotImplementedError("additional residuals belong to the separate_encoder variant")
+        out = self.forward_sources([sample], timestep, encoder_hidden_states)
+        if not return_dict:
+            return (out,)
+        return UNetOutput(sample=out)
+
+    @torch.no_grad()
+    def forward_sources(self, sources, timestep, encoder_hidden_states=None):
+        """forward() on the channel concatenation of up to three NCHW tensors without
+        materialising it (the sampler's ``torch.cat([x_t, rgb, cond], 1)``,
+        trainers_ldm_cond.py:1134-1141, is folded into the NCHW->NHWC gather of conv_in)."""
+        P = self.prepare()
+        dt = self.dtype
+        sample = sources[0]
+        dev = sample.device
+        B, _, H, W = sample.shape
+        Cin = sum(s.shape[1] for s in sources)
+        if Cin != self.conv_in.in_channels:
+            raise ValueError(f"UNet expects {self.conv_in.in_channels} input channels, got {Cin}")
+        # 1. time (unet.py:301-307): timesteps.expand(B) -> sinusoid -> MLP; SiLU(emb) feeds
+        #    the batched time_emb_proj GEMM (fp32 out, added in the conv1 epilogues)
+        if not torch.is_tensor(timestep):
+            timestep = torch.tensor([timestep], device=dev)
+        t = timestep.reshape(-1).to(device=dev, dtype=torch.float32)
+        emb = K.timestep_proj(t, B, P["freqs"], self.time_proj.num_channels, self.time_proj.flip_sin_to_cos, dt)
+        emb = K.linear(P["lin1"], emb, act=K.ACT_SILU)
+        emb = K.linear(P["lin2"], emb, act=K.ACT_SILU)                   # = SiLU(time_embedding(t))
+        temb_all = K.linear(P["temb_proj"], emb, out_dtype=torch.float32)  # [B, sum Cout]
+        # 3. conv_in (unet.py:357)
+        x = K.nchw_to_nhwc(sources, P["cin_pad"], dt)
+        x = K.conv2d(P["conv_in"], x, B, H, W)
+        skips = [(x, H, W)]
+        for blk in self.down_blocks:
+            for j, r in enumerate(blk.resnets):
+                x = self._resnet(P, r, (x, None), B, H, W, temb_all)
+                if blk.has_cross_attention:
+                    x = self._transformer(P, blk.attentions[j], x, B, H, W, encoder_hidden_states)
+                skips.append((x, H, W))
+            if blk.downsamplers is not None:
+                x = K.conv2d(P[id(blk.downsamplers[0])], x, B, H, W, stride=2)
+                H, W = (H + 1) // 2, (W + 1) // 2
+                skips.append((x, H, W))
+        mb = self.mid_block
+        x = self._resnet(P, mb.resnets[0], (x, None), B, H, W, temb_all)
+        x = self._transformer(P, mb.attentions[0], x, B, H, W, encoder_hidden_states)
+        x = self._resnet(P, mb.resnets[1], (x, None), B, H, W, temb_all)
+        for blk in self.up_blocks:
+            for j, r in enumerate(blk.resnets):
+                s, sh, sw = skips.pop()
+                assert (sh, sw) == (H, W)
+                x = self._resnet(P, r, (x, s), B, H, W, temb_all)      # cat([x, skip]) read in place
+                if blk.has_cross_attention:
+                    x = self._transformer(P, blk.attentions[j], x, B, H, W, encoder_hidden_states)
+            if blk.upsamplers is not None:
+                x = K.conv2d(P[id(blk.upsamplers[0])], x, B, H, W, upsample=True)
+                H, W = 2 * H, 2 * W
+        x = K.group_norm(x, B, H * W, self.conv_norm_out.num_groups, *P["out_norm"], self.conv_norm_out.eps,
+                         K.ACT_SILU)
+        return K.conv2d(P["conv_out"], x, B, H, W, out_layout=K.OUT_NCHW)
+
+
+def _remap_legacy_keys(sd):
+    """Older diffusers checkpoints name the attention output projection ``to_out.0`` already;
+    the pre-0.14 ``attentions.*.query/key/value/proj_attn`` names only occur in VAE mid blocks,
+    which are not part of this UNet.  Kept as the single place to add remaps."""
+    return sd

@@ -1,0 +1,501 @@
+"""ctypes binding of lib/libldmseg_hip.so (C ABI: include/ldmseg_hip.h) + tensor-level wrappers.
+
+Every op here launches a hand-written gfx950 kernel on the current torch stream.  There is
+no fallback: if the library is missing, or a tensor is not on the GPU, the call raises.
+Host-side checks (device, dtype, contiguity, shapes) run before any launch so that a bad
+call can never reach the GPU as an out-of-bounds kernel.
+"""
+import ctypes
+import math
+import os
+import threading
+
+import torch
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libldmseg_hip.so")
+
+F32, BF16 = 0, 1
+OUT_NHWC, OUT_NCHW, OUT_GEGLU, OUT_SHUFFLE2 = 0, 1, 2, 3
+ACT_NONE, ACT_SILU = 0, 1
+PRED = {"epsilon": 0, "sample": 1, "v_prediction": 2}
+POST_ACT = {"none": 0, "tanh": 1, "sigmoid": 2, "clip": 3}
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_i64 = ctypes.c_int64
+
+
+class ConvParams(ctypes.Structure):
+    _fields_ = [("a0", _vp), ("a1", _vp), ("c0", _i), ("c1", _i), ("batch", _i), ("h_in", _i), ("w_in", _i),
+                ("h_out", _i), ("w_out", _i), ("ksize", _i), ("stride", _i), ("upsample", _i), ("w", _vp),
+                ("n", _i), ("kpad", _i), ("bias", _vp), ("temb", _vp), ("temb_stride", _i), ("residual", _vp),
+                ("out", _vp), ("out_layout", _i), ("act", _i), ("dtype", _i), ("out_f32", _i)]
+
+
+class AttnParams(ctypes.Structure):
+    _fields_ = [("q", _vp), ("k", _vp), ("v", _vp), ("o", _vp), ("q_stride", _i), ("k_stride", _i),
+                ("v_stride", _i), ("o_stride", _i), ("batch", _i), ("heads", _i), ("head_dim", _i),
+                ("n_q", _i), ("n_kv", _i), ("scale", _f), ("dtype", _i)]
+
+
+class DdimParams(ctypes.Structure):
+    _fields_ = [("model_output", _vp), ("mo_dtype", _i), ("sample", _vp), ("x_dtype", _i), ("prev", _vp),
+                ("x0", _vp), ("out_dtype", _i), ("n", _i64), ("t", _vp), ("alphas_cumprod", _vp),
+                ("final_alpha_cumprod", _f), ("step_ratio", _i), ("prediction_type", _i), ("clip_sample", _i),
+                ("clip_range", _f), ("use_clipped_model_output", _i), ("num_train_timesteps", _i)]
+
+
+EXPORTS = {
+    "ldm_conv2d": (_i, [ctypes.POINTER(ConvParams), _vp]),
+    "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
+    "ldm_group_norm_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
+    "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _i, _vp]),
+    "ldm_layer_norm": (_i, [_vp, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp]),
+    "ldm_timestep_proj": (_i, [_vp, _i, _i, _vp, _i, _i, _vp, _i, _vp]),
+    "ldm_ddim_step": (_i, [ctypes.POINTER(DdimParams), _vp]),
+    "ldm_ddim_add_noise": (_i, [_vp, _vp, _vp, _vp, _i, _f, _i, _i64, _vp, _i, _vp]),
+    "ldm_ddim_remove_noise": (_i, [_vp, _vp, _vp, _vp, _i, _f, _i, _i64, _vp, _i, _vp]),
+    "ldm_bit_encode": (_i, [_vp, _i, _i64, _i, _i64, _f, _vp, _vp, _vp]),
+    "ldm_bit_decode": (_i, [_vp, _i, _i, _i64, _i, _vp, _i, _vp]),
+    "ldm_nchw_to_nhwc": (_i, [_vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp]),
+    "ldm_resize_bilinear": (_i, [_vp, _i, _i, _i, _i, _i, _f, _f, _f, _f, _vp, _i, _i, _vp]),
+    "ldm_gaussian_posterior": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
+    "ldm_status_string": (ctypes.c_char_p, [_i]),
+    "ldm_abi_version": (_i, []),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load_library(path=LIB_PATH):
+    """Load the HIP library (no GPU needed to load it; kernels need one to run)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise RuntimeError(f"ldmseg HIP library not found at {path}: run "
+                                   f"`python video-latent-diffusion-panoptic-segmentation_amd/build.py` "
+                                   f"(or __graft_entry__.build()) first")
+            lib = ctypes.CDLL(path)
+            for name, (res, args) in EXPORTS.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def _check(status, what):
+    if status != 0:
+        msg = load_library().ldm_status_string(status).decode()
+        raise RuntimeError(f"{what} failed: {msg} (status {status})")
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise TypeError(f"unsupported dtype {dt}: the HIP path computes in float32 or bfloat16")
+
+
+def _stream(t):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("ldmseg HIP ops take GPU tensors only (no CPU fallback); got a tensor on "
+                               f"{t.device}")
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _contig(t, name):
+    if t is not None and not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+# ======================================================================================
+# launch profiler (bench.py roofline): HIP events around each launch on its stream
+# ======================================================================================
+class LaunchProfiler:
+    """Records (family, algorithmic flops, algorithmic bytes, start/end events) per launch."""
+
+    def __init__(self):
+        self.records = []
+
+    def start(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def stop(self, family, flops, nbytes, ev0):
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self.records.append((family, flops, nbytes, ev0, ev1))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        fam = {}
+        for f, fl, by, e0, e1 in self.records:
+            d = fam.setdefault(f, dict(launches=0, ms=0.0, flops=0.0, bytes=0.0))
+            d["launches"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["flops"] += fl
+            d["bytes"] += by
+        return fam
+
+
+_PROFILER = None
+
+
+def set_profiler(p):
+    global _PROFILER
+    _PROFILER = p
+
+
+def _prof_start():
+    return _PROFILER.start() if _PROFILER is not None else None
+
+
+def _prof_stop(ev0, family, flops, nbytes):
+    if ev0 is not None:
+        _PROFILER.stop(family, flops, nbytes, ev0)
+
+
+# ======================================================================================
+# packed weights
+# ======================================================================================
+def _kpad(k):
+    return (k + 63) // 64 * 64
+
+
+class PackedConv:
+    """A conv/linear weight packed for ldm_conv2d: [n][kpad], k = (ky, kx, c) tap-major.
+
+    ``cin_pad`` zero-pads the input channels (e.g. conv_in's 8/12 -> 16 so every 16-byte
+    chunk of the NHWC input is one tap).  ``geglu`` interleaves the hidden/gate halves of a
+    GEGLU projection in 16-column blocks; ``shuffle2`` packs a ConvTranspose2d(k=2, s=2).
+    """
+
+    def __init__(self, weight, bias, dtype, cin_pad=None, geglu=False, shuffle2=False):
+        w = weight.detach()
+        if shuffle2:                       # ConvTranspose2d weight [cin, cout, 2, 2]
+            cin, cout = w.shape[0], w.shape[1]
+            wp = w.permute(2, 3, 1, 0).reshape(4 * cout, cin)          # n = (dy*2+dx)*cout + co
+            b = None if bias is None else bias.detach().float().repeat(4)
+            self.ksize, self.cin, self.n = 1, cin, 4 * cout
+            self.cin_real = cin
+        else:
+            if w.ndim == 2:
+                w = w[:, :, None, None]
+            cout, cin, kh, kw = w.shape
+            assert kh == kw and kh in (1, 3), "only 1x1 / 3x3 kernels are on the path"
+            cp = cin_pad or cin
+            self.cin_real = cin
+            if cp != cin:
+                w = torch.nn.functional.pad(w, (0, 0, 0, 0, 0, cp - cin))
+            wp = w.permute(0, 2, 3, 1).reshape(cout, kh * kw * cp)
+            b = None if bias is None else bias.detach().float()
+            if geglu:
+                half = cout // 2
+                assert half % 16 == 0, "GEGLU packing needs 16-aligned halves"
+                wh, wg = wp[:half].reshape(half // 16, 16, -1), wp[half:].reshape(half // 16, 16, -1)
+                wp = torch.stack([wh, wg], dim=1).reshape(cout, -1)
+                if b is not None:
+                    bh, bg = b[:half].reshape(-1, 16), b[half:].reshape(-1, 16)
+                    b = torch.stack([bh, bg], dim=1).reshape(-1)
+            self.ksize, self.cin, self.n = kh, cp, cout
+        K = wp.shape[1]
+        self.kpad = _kpad(K)
+        packed = torch.zeros(wp.shape[0], self.kpad, dtype=dtype, device=wp.device)
+        packed[:, :K] = wp.to(dtype)
+        self.w = packed.contiguous()
+        self.bias = None if b is None else b.contiguous()
+        self.dtype = dtype
+        self.geglu = geglu
+        self.shuffle2 = shuffle2
+
+
+def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False, temb=None, temb_stride=0,
+           residual=None, out=None, out_layout=OUT_NHWC, act=ACT_NONE, out_dtype=None):
+    """Run ldm_conv2d.  x0/x1: NHWC [batch, h, w, c] (any contiguous view with that numel)."""
+    lib = load_library()
+    _gpu(x0, x1, pc.w, temb, residual, out)
+    c0 = x0.numel() // (batch * h * w)
+    c1 = 0 if x1 is None else x1.numel() // (batch * h * w)
+    if c0 * batch * h * w != x0.numel() or (x1 is not None and c1 * batch * h * w != x1.numel()):
+        raise ValueError("input numel does not match batch*h*w*c")
+    if c0 + c1 != pc.cin:
+        raise ValueError(f"conv expects {pc.cin} input channels, got {c0}+{c1}")
+    for t, nm in ((x0, "x0"), (x1, "x1"), (residual, "residual")):
+        _contig(t, nm)
+    if x0.dtype != pc.dtype or (x1 is not None and x1.dtype != pc.dtype):
+        raise TypeError(f"conv input dtype {x0.dtype} != packed weight dtype {pc.dtype}")
+    if pc.ksize == 1:
+        ho, wo = h, w
+    elif upsample:
+        ho, wo = 2 * h, 2 * w
+    else:
+        ho, wo = (h + 2 - 3) // stride + 1, (w + 2 - 3) // stride + 1
+    n = pc.n
+    if out_layout == OUT_GEGLU:
+        shape = (batch, ho, wo, n // 2)
+    elif out_layout == OUT_NCHW:
+        shape = (batch, n, ho, wo)
+    elif out_layout == OUT_SHUFFLE2:
+        shape = (batch, 2 * ho, 2 * wo, n // 4)
+    else:
+        shape = (batch, ho, wo, n)
+    odt = out_dtype or pc.dtype
+    if out is None:
+        out = torch.empty(shape, dtype=odt, device=x0.device)
+    elif out.numel() != math.prod(shape) or out.dtype != odt:
+        raise ValueError("preallocated out has the wrong size / dtype")
+    if residual is not None and (residual.numel() != out.numel() or residual.dtype != pc.dtype):
+        raise ValueError("residual must match the output size and the compute dtype")
+    if temb is not None:
+        # temb may be a column slice [B, n:] of the batched time_emb_proj output: element
+        # (b, j) lives at temb.data_ptr() + (b * temb_stride + j) * 4
+        if temb.dtype != torch.float32 or temb.ndim != 2 or temb.stride(-1) != 1 or temb.shape[0] != batch:
+            raise ValueError("temb must be an fp32 [batch, >=n] row-major view")
+        if temb.shape[1] < n or temb.stride(0) != temb_stride:
+            raise ValueError("temb view narrower than n or stride mismatch")
+    p = ConvParams(_ptr(x0), _ptr(x1), c0, c1, batch, h, w, ho, wo, pc.ksize, stride, int(upsample), _ptr(pc.w),
+                   n, pc.kpad, _ptr(pc.bias), _ptr(temb), temb_stride, _ptr(residual), _ptr(out), out_layout, act,
+                   dtype_code(pc.dtype), int(odt == torch.float32 and pc.dtype != torch.float32))
+    ev = _prof_start()
+    _check(lib.ldm_conv2d(ctypes.byref(p), _stream(x0)), "ldm_conv2d")
+    if ev is not None:
+        M = batch * ho * wo
+        flops = 2.0 * M * n * pc.ksize * pc.ksize * pc.cin_real
+        nbytes = (x0.numel() + (0 if x1 is None else x1.numel()) + pc.w.numel()) * x0.element_size() + \
+            out.numel() * out.element_size() + (0 if residual is None else residual.numel() * residual.element_size())
+        _prof_stop(ev, "igemm", flops, nbytes)
+    return out
+
+
+def linear(pc: PackedConv, x, **kw):
+    """x [..., K] rows -> [..., N] (a 1x1 conv over rows)."""
+    rows = x.numel() // x.shape[-1]
+    y = conv2d(pc, x, rows, 1, 1, **kw)
+    if kw.get("out_layout", OUT_NHWC) == OUT_GEGLU:
+        return y.view(*x.shape[:-1], pc.n // 2)
+    return y.view(*x.shape[:-1], y.shape[-1])
+
+
+# ======================================================================================
+# attention / norms
+# ======================================================================================
+def attention(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_stride, out=None, scale=None):
+    lib = load_library()
+    _gpu(q, k, v, out)
+    C = heads * head_dim
+    if out is None:
+        out = torch.empty(batch, n_q, C, dtype=q.dtype, device=q.device)
+    if not (q.dtype == k.dtype == v.dtype == out.dtype):
+        raise TypeError("q/k/v/out dtypes differ")
+    for t, stride, n in ((q, q_stride, n_q), (k, k_stride, n_kv), (v, v_stride, n_kv)):
+        need = ((batch - 1) * n + (n - 1)) * stride + C
+        if t.storage_offset() + need > t.untyped_storage().nbytes() // t.element_size():
+            raise ValueError("attention operand too small for the given strides")
+    p = AttnParams(_ptr(q), _ptr(k), _ptr(v), _ptr(out), q_stride, k_stride, v_stride, C, batch, heads, head_dim,
+                   n_q, n_kv, float(scale if scale is not None else head_dim ** -0.5), dtype_code(q.dtype))
+    ev = _prof_start()
+    _check(lib.ldm_attention(ctypes.byref(p), _stream(q)), "ldm_attention")
+    _prof_stop(ev, "attention", 4.0 * batch * heads * n_q * n_kv * head_dim,
+               (2 * batch * n_q * C + 2 * batch * n_kv * C) * q.element_size())
+    return out
+
+
+def group_norm(x0, batch, hw, groups, gamma, beta, eps, act=ACT_NONE, x1=None, out=None):
+    """GroupNorm over NHWC [batch, hw, c0 (+c1)] -> contiguous NHWC [batch, hw, c0+c1]."""
+    lib = load_library()
+    _gpu(x0, x1, gamma, beta, out)
+    _contig(x0, "x0")
+    _contig(x1, "x1")
+    c0 = x0.numel() // (batch * hw)
+    c1 = 0 if x1 is None else x1.numel() // (batch * hw)
+    C = c0 + c1
+    if gamma.numel() != C or beta.numel() != C or gamma.dtype != torch.float32 or beta.dtype != torch.float32:
+        raise ValueError("gamma/beta must be fp32 [C]")
+    if out is None:
+        out = torch.empty(batch, hw, C, dtype=x0.dtype, device=x0.device)
+    ws = torch.empty(int(lib.ldm_group_norm_workspace_bytes(batch, hw, C)), dtype=torch.uint8, device=x0.device)
+    ev = _prof_start()
+    _check(lib.ldm_group_norm(_ptr(x0), _ptr(x1), c0, c1, batch, hw, groups, _ptr(gamma), _ptr(beta), float(eps),
+                              act, _ptr(out), _ptr(ws), dtype_code(x0.dtype), _stream(x0)), "ldm_group_norm")
+    _prof_stop(ev, "group_norm", 0.0, 3.0 * out.numel() * out.element_size())
+    return out
+
+
+def layer_norm(x, gamma, beta, eps, act=ACT_NONE, out=None):
+    lib = load_library()
+    _gpu(x, gamma, beta, out)
+    _contig(x, "x")
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if out is None:
+        out = torch.empty_like(x)
+    ev = _prof_start()
+    _check(lib.ldm_layer_norm(_ptr(x), rows, C, _ptr(gamma), _ptr(beta), float(eps), act, _ptr(out),
+                              dtype_code(x.dtype), _stream(x)), "ldm_layer_norm")
+    _prof_stop(ev, "layer_norm", 0.0, 2.0 * out.numel() * out.element_size())
+    return out
+
+
+def timestep_proj(t_f32, batch, freqs, dim, flip_sin_to_cos, dtype):
+    lib = load_library()
+    _gpu(t_f32, freqs)
+    if t_f32.dtype != torch.float32 or t_f32.numel() not in (1, batch):
+        raise ValueError("timesteps must be fp32 with 1 or batch elements")
+    out = torch.empty(batch, dim, dtype=dtype, device=t_f32.device)
+    _check(lib.ldm_timestep_proj(_ptr(t_f32), t_f32.numel(), batch, _ptr(freqs), dim, int(flip_sin_to_cos),
+                                 _ptr(out), dtype_code(dtype), _stream(t_f32)), "ldm_timestep_proj")
+    return out
+
+
+# ======================================================================================
+# DDIM, codec, layout helpers
+# ======================================================================================
+def ddim_step(model_output, sample, t_dev, alphas_cumprod_dev, final_alpha, step_ratio, prediction_type,
+              clip_sample, clip_range, use_clipped, out_dtype, want_prev=True, want_x0=True):
+    lib = load_library()
+    _gpu(model_output, sample, t_dev, alphas_cumprod_dev)
+    _contig(model_output, "model_output")
+    _contig(sample, "sample")
+    if model_output.numel() != sample.numel():
+        raise ValueError("model_output and sample sizes differ")
+    if t_dev.dtype != torch.int64 or t_dev.numel() != 1:
+        raise ValueError("t must be a single int64 device element")
+    prev = torch.empty(sample.shape, dtype=out_dtype, device=sample.device) if want_prev else None
+    x0 = torch.empty(sample.shape, dtype=out_dtype, device=sample.device) if want_x0 else None
+    p = DdimParams(_ptr(model_output), dtype_code(model_output.dtype), _ptr(sample), dtype_code(sample.dtype),
+                   _ptr(prev), _ptr(x0), dtype_code(out_dtype), sample.numel(), _ptr(t_dev), _ptr(alphas_cumprod_dev),
+                   float(final_alpha), int(step_ratio), PRED[prediction_type], int(clip_sample), float(clip_range),
+                   int(use_clipped), alphas_cumprod_dev.numel())
+    _check(lib.ldm_ddim_step(ctypes.byref(p), _stream(sample)), "ldm_ddim_step")
+    return prev, x0
+
+
+def ddim_add_noise(x0, noise, t_dev, ac_dev, scale):
+    lib = load_library()
+    _gpu(x0, noise, t_dev, ac_dev)
+    _contig(x0, "x0")
+    _contig(noise, "noise")
+    B = x0.shape[0]
+    if t_dev.numel() != B or t_dev.dtype != torch.int64 or noise.shape != x0.shape or noise.dtype != x0.dtype:
+        raise ValueError("add_noise: timesteps must be int64 [B]; noise must match x0")
+    out = torch.empty_like(x0)
+    _check(lib.ldm_ddim_add_noise(_ptr(x0), _ptr(noise), _ptr(t_dev), _ptr(ac_dev), ac_dev.numel(), float(scale), B,
+                                  x0.numel() // B, _ptr(out), dtype_code(x0.dtype), _stream(x0)), "ldm_ddim_add_noise")
+    return out
+
+
+def ddim_remove_noise(xt, noise, t_dev, ac_dev, scale):
+    lib = load_library()
+    _gpu(xt, noise, t_dev, ac_dev)
+    _contig(xt, "xt")
+    _contig(noise, "noise")
+    B = xt.shape[0]
+    if t_dev.numel() != B or t_dev.dtype != torch.int64 or noise.shape != xt.shape or noise.dtype != xt.dtype:
+        raise ValueError("remove_noise: timesteps must be int64 [B]; noise must match xt")
+    out = torch.empty_like(xt)
+    _check(lib.ldm_ddim_remove_noise(_ptr(xt), _ptr(noise), _ptr(t_dev), _ptr(ac_dev), ac_dev.numel(), float(scale), B,
+                                     xt.numel() // B, _ptr(out), dtype_code(xt.dtype), _stream(xt)),
+           "ldm_ddim_remove_noise")
+    return out
+
+
+def bit_encode(ids, n, ignore_label, fill_value):
+    """ids int64 [..., H, W] (GPU) -> (planes fp32 [..., n, H, W], ignore mask bool [..., H, W])."""
+    lib = load_library()
+    _gpu(ids)
+    if ids.dtype != torch.int64:
+        raise TypeError("ids must be int64")
+    ids = ids.contiguous()
+    H, W = ids.shape[-2], ids.shape[-1]
+    batch = math.prod(ids.shape[:-2])
+    planes = torch.empty(*ids.shape[:-2], n, H, W, dtype=torch.float32, device=ids.device)
+    mask = torch.empty(ids.shape, dtype=torch.bool, device=ids.device)
+    _check(lib.ldm_bit_encode(_ptr(ids), batch, H * W, n, int(ignore_label), float(fill_value), _ptr(planes),
+                              _ptr(mask), _stream(ids)), "ldm_bit_encode")
+    return planes, mask
+
+
+def bit_decode(planes, drop_31=True):
+    """planes [..., n, H, W] (GPU, fp32/bf16) -> ids int64 [..., H, W]."""
+    lib = load_library()
+    _gpu(planes)
+    planes = planes.contiguous()
+    n, H, W = planes.shape[-3], planes.shape[-2], planes.shape[-1]
+    batch = math.prod(planes.shape[:-3]) if planes.ndim > 3 else 1
+    ids = torch.empty(*planes.shape[:-3], H, W, dtype=torch.int64, device=planes.device)
+    _check(lib.ldm_bit_decode(_ptr(planes), batch, n, H * W, int(drop_31), _ptr(ids), dtype_code(planes.dtype),
+                              _stream(planes)), "ldm_bit_decode")
+    return ids
+
+
+def nchw_to_nhwc(sources, c_pad, dtype):
+    """Gather up to three NCHW tensors [B, c_i, H, W] into one NHWC [B, H, W, c_pad] tensor."""
+    lib = load_library()
+    srcs = [s.contiguous() for s in sources if s is not None]
+    _gpu(*srcs)
+    if not 1 <= len(srcs) <= 3:
+        raise ValueError("1..3 sources")
+    B, _, H, W = srcs[0].shape
+    for s in srcs:
+        if s.shape[0] != B or s.shape[2:] != (H, W):
+            raise ValueError("sources must share batch and spatial size")
+    args = []
+    for i in range(3):
+        if i < len(srcs):
+            s = srcs[i]
+            args += [_ptr(s), s.shape[1], dtype_code(s.dtype)]
+        else:
+            args += [None, 0, 0]
+    out = torch.empty(B, H, W, c_pad, dtype=dtype, device=srcs[0].device)
+    _check(lib.ldm_nchw_to_nhwc(*args, B, H * W, c_pad, _ptr(out), dtype_code(dtype), _stream(srcs[0])),
+           "ldm_nchw_to_nhwc")
+    return out
+
+
+def resize_bilinear(x, size=None, scale_factor=None, mul=1.0, add=0.0, out_dtype=None):
+    """F.interpolate(x, size|scale_factor, mode='bilinear', align_corners=False) * mul + add (NCHW)."""
+    lib = load_library()
+    _gpu(x)
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    if size is not None:
+        ho, wo = (size, size) if isinstance(size, int) else tuple(size)
+        sh, sw = H / ho, W / wo
+    else:
+        sfh, sfw = (scale_factor, scale_factor) if not isinstance(scale_factor, (tuple, list)) else scale_factor
+        ho, wo = int(math.floor(H * sfh)), int(math.floor(W * sfw))
+        sh, sw = 1.0 / sfh, 1.0 / sfw
+    odt = out_dtype or x.dtype
+    out = torch.empty(B, C, ho, wo, dtype=odt, device=x.device)
+    _check(lib.ldm_resize_bilinear(_ptr(x), B * C, H, W, ho, wo, float(sh), float(sw), float(mul), float(add),
+                                   _ptr(out), dtype_code(x.dtype), dtype_code(odt), _stream(x)), "ldm_resize_bilinear")
+    return out
+
+
+def gaussian_posterior(moments, clamp_output, act_fn):
+    """NCHW moments [B, 2L, H, W] -> (mean, logvar, std, var) fp32 [B, L, H, W]."""
+    lib = load_library()
+    _gpu(moments)
+    moments = moments.contiguous()
+    B, C2, H, W = moments.shape
+    L = C2 // 2
+    outs = [torch.empty(B, L, H, W, dtype=torch.float32, device=moments.device) for _ in range(4)]
+    _check(lib.ldm_gaussian_posterior(_ptr(moments), B, H * W, L, int(clamp_output), POST_ACT[act_fn],
+                                      *[_ptr(o) for o in outs], dtype_code(moments.dtype), _stream(moments)),
+           "ldm_gaussian_posterior")
+    return tuple(outs)
