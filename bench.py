@@ -66,7 +66,14 @@ def roofline(unet, stepper, ts, nsteps, dtype):
     finally:
         K.set_profiler(None)
     fam = prof.summary()
-    per_step = {k: dict(launches=v["launches"] // nsteps, ms=round(v["ms"] / nsteps, 4),
+    if os.environ.get("LDM_BENCH_DETAIL"):
+        det = prof.summary(by_detail=True)
+        print(f"{'kernel':10s} {'shape':44s} {'n':>3s} {'ms':>8s} {'TF/s':>7s} {'GB/s':>7s}", file=sys.stderr)
+        for (f, s), v in sorted(det.items(), key=lambda kv: -kv[1]["ms"])[:40]:
+            ms = v["ms"] / nsteps
+            print(f"{f:10s} {s:44s} {v['launches'] // nsteps:3d} {ms:8.3f} "
+                  f"{v['flops'] / nsteps / ms / 1e9:7.1f} {v['bytes'] / nsteps / ms / 1e6:7.1f}", file=sys.stderr)
+    per_step ={k: dict(launches=v["launches"] // nsteps, ms=round(v["ms"] / nsteps, 4),
                         gflop=round(v["flops"] / nsteps / 1e9, 2), mb=round(v["bytes"] / nsteps / 1e6, 2))
                 for k, v in fam.items()}
     dom = max(fam, key=lambda k: fam[k]["ms"])

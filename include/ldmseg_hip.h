@@ -76,8 +76,14 @@ typedef struct {
   int act;                 /* LDM_ACT_* applied after bias/temb, before residual */
   int dtype;               /* A / W / residual dtype */
   int out_f32;             /* 1: out is fp32 regardless of dtype */
+  void* workspace;         /* split-K fp32 slab, >= ldm_conv2d_workspace_bytes(p) bytes (or NULL if 0) */
+  int64_t workspace_bytes;
+  float* gn_partial;       /* optional: per 64-row chunk, per channel (sum, sumsq) of the output,
+                              [M/64][n] float2 — the GroupNorm statistics input (NHWC, M % 64 == 0) */
 } ldm_conv_params;
 
+/* Deep-K / few-tile shapes are split over K into an fp32 slab; this returns its size (0: none). */
+size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* p);
 int ldm_conv2d(const ldm_conv_params* p, ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
@@ -102,12 +108,15 @@ int ldm_attention(const ldm_attn_params* p, ldm_stream_t stream);
  * concatenated sources (the up-block [hidden || skip] concat is never materialised).
  * Replaces: ResnetBlock2D norm1/norm2 + SiLU (eps 1e-5), Transformer2DModel.norm (eps 1e-6),
  * conv_norm_out + conv_act (unet.py:428-430), GeneralVAESeg GroupNorm (vae.py:163,235).
+ * stats0/stats1: the per-64-pixel-chunk channel (sum, sumsq) partials [batch*hw/64][c_i] float2
+ * that ldm_conv2d's epilogue wrote for x0 / x1 (gn_partial), or NULL to compute them here.
  * workspace: >= ldm_group_norm_workspace_bytes(batch, hw, c0 + c1) bytes of device memory.
  * ------------------------------------------------------------------------------------- */
 size_t ldm_group_norm_workspace_bytes(int batch, int hw, int channels);
 int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
                    const float* gamma, const float* beta, float eps, int act, void* out,
-                   void* workspace, int dtype, ldm_stream_t stream);
+                   const float* stats0, const float* stats1, void* workspace, int dtype,
+                   ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_layer_norm — LayerNorm over the channel dimension of [rows][c] (NHWC pixels or tokens).

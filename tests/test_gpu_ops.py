@@ -40,6 +40,9 @@ CONV_CASES = [
     ("1x1_concat", 2, 128, 64, 8, 8, 64, 1, 1, False),
     ("odd_n", 1, 32, 0, 5, 5, 4, 3, 1, False),
     ("unet_l0", 1, 320, 0, 64, 64, 320, 3, 1, False),
+    ("unet_l3_splitk", 8, 1280, 0, 8, 8, 1280, 3, 1, False),       # few tiles, deep K -> split-K
+    ("unet_up_concat_splitk", 4, 1280, 640, 16, 16, 1280, 3, 1, False),
+    ("concat_unaligned", 2, 40, 24, 6, 6, 16, 3, 1, False),         # per-lane source select
 ]
 
 
@@ -72,6 +75,32 @@ def test_conv2d(case, dt):
     out2 = K.conv2d(pc, x0, B, H, W, x1=x1, stride=s, upsample=up, out_layout=K.OUT_NCHW)
     ref2 = F.conv2d(xr, w, b, stride=s, padding=k // 2)
     assert rel_err(out2, ref2) < tol(dt)
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("B,H,C,Co,G,split", [(2, 32, 128, 320, 32, False), (8, 8, 1280, 1280, 32, True),
+                                               (1, 16, 64, 64, 16, False)])
+def test_conv_epilogue_groupnorm_stats(B, H, C, Co, G, split, dt):
+    """Producer-epilogue (sum, sumsq) partials feed GroupNorm: no statistics pass, same result.
+    Also across a concat whose second half carries its own producer statistics."""
+    torch.manual_seed(8)
+    x = torch.randn(B, C, H, H)
+    w = torch.randn(Co, C, 3, 3) / (3 * C ** 0.5)
+    b = torch.randn(Co)
+    y_ref = F.conv2d(x, w, b, padding=1)
+    pc = K.PackedConv(w.to(DEV), b.to(DEV), dt)
+    y = K.conv2d(pc, x.permute(0, 2, 3, 1).contiguous().to(DEV, dt), B, H, H, gn_stats=True)
+    assert K.gn_stats_of(y) is not None
+    gam, bet = torch.randn(Co), torch.randn(Co)
+    out = K.group_norm(y, B, H * H, G, gam.to(DEV), bet.to(DEV), 1e-5, K.ACT_SILU)
+    ref = F.silu(F.group_norm(y_ref, G, gam, bet, 1e-5))
+    assert rel_err(out.view(B, H, H, -1).permute(0, 3, 1, 2), ref) < (2e-4 if dt == torch.float32 else 3e-2)
+    # concat [y || y2] where y2 has producer stats too
+    y2 = K.conv2d(pc, x.permute(0, 2, 3, 1).contiguous().to(DEV, dt), B, H, H, act=K.ACT_SILU, gn_stats=True)
+    gam2, bet2 = torch.randn(2 * Co), torch.randn(2 * Co)
+    out2 = K.group_norm(y, B, H * H, G, gam2.to(DEV), bet2.to(DEV), 1e-6, x1=y2)
+    ref2 = F.group_norm(torch.cat([y_ref, F.silu(y_ref)], 1), G, gam2, bet2, 1e-6)
+    assert rel_err(out2.view(B, H, H, -1).permute(0, 3, 1, 2), ref2) < (2e-4 if dt == torch.float32 else 3e-2)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

@@ -3,14 +3,23 @@
 // One kernel covers every matmul-shaped op of the denoising path: 3x3 convs (stride 1/2,
 // optional nearest-2x upsampled input, optional two-source channel concat), 1x1 convs /
 // linears, and the ConvTranspose k2s2 of the seg-VAE decoder (pixel-shuffle epilogue).
-//   rows m   = output pixels (b, oy, ox)              [NHWC activations]
-//   cols n   = output channels                         [weights packed n-major, K contiguous]
-//   k        = (ky, kx, c) tap-major                    [K tiles of 128 bytes]
-// Tile BM x BN x (128 B of K); 256 threads = 2x2 waves, each wave (BM/2) x (BN/2) built from
-// 16x16 MFMA fragments.  Operands are staged global -> registers -> LDS (XOR-swizzled 16-B
-// chunks, conflict-free ds_read_b128), double-buffered with one barrier per K tile; the
-// register stage is where conv zero-padding, upsample and concat addressing happen.
-// The same code runs bf16 (v_mfma_f32_16x16x32_bf16) and exact fp32 (v_mfma_f32_16x16x4_f32).
+//   rows m = output pixels (b, oy, ox) of NHWC activations
+//   cols n = output channels; weights pre-packed [n][kpad], K contiguous
+//   k      = (ky, kx, c) tap-major, consumed in K tiles of 128 bytes
+// Main loop: block tile BM x BN, 256 threads = 2x2 waves, wave tile (BM/2) x (BN/2) of 16x16
+// MFMA fragments.  Operands: buffer_load_dwordx4 (raw buffer with hardware range check: conv
+// zero padding and tile edges are an out-of-range offset that reads 0 — no branches) into
+// registers, then XOR-swizzled 16-B chunks in LDS (conflict-free ds_read_b128), double
+// buffered, one barrier per K tile; the next tile's global loads are in flight during the
+// current tile's MFMAs.  Blocks are remapped so the N tiles of one M panel run back to back
+// on one XCD (shared L2).  Deep-K / few-tile shapes (the 8x8 and 16x16 UNet levels) split K
+// over blocks into an fp32 slab reduced by a second kernel.
+// Epilogue: raw accumulators are staged through LDS and written back as full coalesced rows
+// (bias, per-(batch, channel) time embedding, SiLU, GEGLU, residual, NHWC / NCHW / pixel
+// shuffle).  Optionally it also emits per-channel (sum, sum of squares) over every 64-row
+// chunk — the GroupNorm statistics of the tensor it just wrote, so the following GroupNorm
+// never re-reads it for statistics.
+// bf16: v_mfma_f32_16x16x32_bf16; fp32: v_mfma_f32_16x16x4_f32 (exact) — same code.
 #include "common.h"
 
 namespace {
@@ -18,10 +27,12 @@ namespace {
 struct ConvArgs {
   const char* a0;
   const char* a1;
+  int a0_bytes, a1_bytes;
   int c0, c1, cin;
-  int batch, h_in, w_in, h_out, w_out, hw_out;
+  int h_in, w_in, h_out, w_out, hw_out;
   int ksize, stride, upsample, pad;
   const char* w;
+  int w_bytes;
   int n, kpad, K;
   const float* bias;
   const float* temb;
@@ -30,12 +41,216 @@ struct ConvArgs {
   char* out;
   int out_layout, act, out_f32;
   int M;
+  int tiles_n, nblk;
+  int mixed_src;      // the concat boundary is not K-tile aligned: per-lane source select
+  int ksplit;         // > 1: write fp32 partials to `partial` [ksplit][M][n]
+  float* partial;
+  float2* gn_part;    // optional [M/64][n] (sum, sumsq) of the final output values
 };
+
+constexpr int kBufFlags = 0x00020000;
+constexpr int kOOB = 0x7ffffff0;  // offset past every num_records: the load returns zeros
 
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
-template <typename T, int BM, int BN>
-__global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs p) {
+__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+// 16 B per lane global -> LDS (LDS address = M0 + 16 * lane).  Inline asm on purpose: hipcc
+// would otherwise drain every in-flight LDS-DMA (vmcnt(0)) before the next ds_read of ANY LDS
+// buffer, serialising the prefetch of tile k+1 with the MFMAs of tile k.  The caller owns the
+// wait: `s_waitcnt vmcnt(0)` + barrier before the buffer is read.  M0 is saved and restored.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, int voff, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds_addr)
+      : "memory");
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(char* base, int64_t idx, const float* v, bool f32out) {
+  if (f32out || sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(base + idx * 4) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    bf16_t h[4] = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    *reinterpret_cast<uint2*>(base + idx * 2) = *reinterpret_cast<const uint2*>(h);
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store1(char* base, int64_t idx, float v, bool f32out) {
+  if (f32out || sizeof(T) == 4) reinterpret_cast<float*>(base)[idx] = v;
+  else reinterpret_cast<bf16_t*>(base)[idx] = f2bf(v);
+}
+template <typename T>
+__device__ __forceinline__ void load4(const char* base, int64_t idx, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    const uint2 rv = *reinterpret_cast<const uint2*>(base + idx * 2);
+    const bf16_t* h = reinterpret_cast<const bf16_t*>(&rv);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = bf2f(h[r]);
+  } else {
+    const float4 rv = *reinterpret_cast<const float4*>(base + idx * 4);
+    v[0] = rv.x; v[1] = rv.y; v[2] = rv.z; v[3] = rv.w;
+  }
+}
+
+// Finish 4 consecutive output channels [n, n+4) of row m from raw accumulators:
+// bias, time embedding, activation, residual, store.  `v` returns the stored values.
+template <typename T>
+__device__ __forceinline__ void finish4(const ConvArgs& p, int m, int n, float* v) {
+  const int N = p.n;
+  const int b = m / p.hw_out;
+  const int pix = m - b * p.hw_out;
+  const bool f32o = p.out_f32 != 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int nn = min(n + r, N - 1);
+    float x = v[r];
+    if (p.bias) x += p.bias[nn];
+    if (p.temb) x += p.temb[(int64_t)b * p.temb_stride + nn];
+    if (p.act == LDM_ACT_SILU) x = silu_f(x);
+    v[r] = x;
+  }
+  if (p.out_layout == LDM_OUT_NCHW) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (n + r >= N) break;
+      const int64_t idx = ((int64_t)b * N + n + r) * p.hw_out + pix;
+      if (p.residual) v[r] += to_f(reinterpret_cast<const T*>(p.residual)[idx]);
+      store1<T>(p.out, idx, v[r], f32o);
+    }
+    return;
+  }
+  int64_t idx;
+  if (p.out_layout == LDM_OUT_NHWC) {
+    idx = (int64_t)m * N + n;
+  } else {  // LDM_OUT_SHUFFLE2: n = (dy*2+dx)*Cout + co -> output pixel (2y+dy, 2x+dx)
+    const int cout = N >> 2;
+    const int qd = n / cout, co = n - qd * cout;
+    const int y = pix / p.w_out, x = pix - y * p.w_out;
+    idx = (((int64_t)b * 2 * p.h_out + 2 * y + (qd >> 1)) * 2 * p.w_out + 2 * x + (qd & 1)) * cout + co;
+  }
+  if (n + 3 < N) {
+    if (p.residual) {
+      float rv[4];
+      load4<T>(p.residual, idx, rv);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += rv[r];
+    }
+    store4<T>(p.out, idx, v, f32o);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (n + r >= N) { v[r] = 0.f; continue; }
+      if (p.residual) v[r] += to_f(reinterpret_cast<const T*>(p.residual)[idx + r]);
+      store1<T>(p.out, idx + r, v[r], f32o);
+    }
+  }
+}
+
+// GEGLU: out[m, oc..oc+3] = (h + bh) * gelu(g + bg); packed columns: 16 hidden then 16 gate
+template <typename T>
+__device__ __forceinline__ void finish_geglu4(const ConvArgs& p, int m, int oc, const float* h, const float* gt) {
+  const int pc = (oc >> 4) * 32 + (oc & 15);
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float hh = h[r] + (p.bias ? p.bias[pc + r] : 0.f);
+    const float gg = gt[r] + (p.bias ? p.bias[pc + 16 + r] : 0.f);
+    v[r] = hh * gelu_f(gg);
+  }
+  store4<T>(p.out, (int64_t)m * (p.n >> 1) + oc, v, p.out_f32 != 0);
+}
+
+// Phase 2 of the epilogue, shared by the fused path (raw values staged in LDS) and the
+// split-K reduction (raw values summed from the fp32 slab).  `raw(r, c4, v)` fills 4 raw
+// values of local row r, local 4-channel chunk c4.  Rows [0, ROWS), channels [0, COLS).
+// Threads sweep (row, chunk) with chunk fastest -> coalesced row segments.
+template <typename T, int ROWS, int COLS, typename RawFn>
+__device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0, RawFn raw, float* red) {
+  constexpr int CW = COLS / 4;           // chunks per row
+  constexpr int RP = 256 / CW;           // rows per pass
+  constexpr int HALVES = ROWS / 64 > 0 ? ROWS / 64 : 1;
+  const int tid = threadIdx.x;
+  const int c4 = tid % CW, r0 = tid / CW;
+  const bool geglu = p.out_layout == LDM_OUT_GEGLU;
+  const bool stats = p.gn_part != nullptr;
+  float s[HALVES][4], q[HALVES][4];
+#pragma unroll
+  for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s[hh][r] = 0.f; q[hh][r] = 0.f; }
+  if (geglu) {
+    constexpr int OCW = CW / 2;          // GEGLU output chunks per row (half width)
+    constexpr int ORP = 256 / OCW;
+    const int oc4 = tid % OCW, or0 = tid / OCW;
+#pragma unroll 2
+    for (int r = or0; r < ROWS; r += ORP) {
+      const int m = m0 + r;
+      const int oc = (n0 >> 1) + 4 * oc4;
+      if (m >= p.M || oc >= (p.n >> 1)) continue;
+      const int lc = 4 * oc4;                       // local output column
+      const int pcl = (lc >> 4) * 32 + (lc & 15);   // local packed column of the hidden half
+      float h[4], gt[4];
+      raw(r, pcl >> 2, h);
+      raw(r, (pcl + 16) >> 2, gt);
+      finish_geglu4<T>(p, m, oc, h, gt);
+    }
+    return;
+  }
+#pragma unroll 2
+  for (int r = r0; r < ROWS; r += RP) {
+    const int m = m0 + r;
+    const int n = n0 + 4 * c4;
+    if (m >= p.M || n >= p.n) continue;
+    float v[4];
+    raw(r, c4, v);
+    finish4<T>(p, m, n, v);
+    if (stats) {
+      const int hh = HALVES > 1 ? (r >> 6) : 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        // statistics of the value as stored (bf16-rounded on the bf16 path)
+        const float x = (sizeof(T) == 2 && !p.out_f32) ? bf2f(f2bf(v[k])) : v[k];
+        s[hh][k] += x;
+        q[hh][k] += x * x;
+      }
+    }
+  }
+  if (!stats) return;
+  // reduce over the RP row-groups that share a chunk column: red[RP][CW][HALVES][4][2]
+  __syncthreads();
+#pragma unroll
+  for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 0] = s[hh][k];
+      red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 1] = q[hh][k];
+    }
+  __syncthreads();
+  for (int e = tid; e < CW * HALVES * 4; e += 256) {
+    const int k = e & 3, hh = (e >> 2) % HALVES, c = e / (4 * HALVES);
+    const int n = n0 + 4 * c + k;
+    const int chunk = (m0 >> 6) + hh;
+    if (n >= p.n || chunk * 64 >= p.M) continue;
+    float a = 0.f, b = 0.f;
+    for (int rg = 0; rg < RP; ++rg) {
+      a += red[(((rg * CW + c) * HALVES + hh) * 4 + k) * 2 + 0];
+      b += red[(((rg * CW + c) * HALVES + hh) * 4 + k) * 2 + 1];
+    }
+    p.gn_part[(int64_t)chunk * p.n + n] = make_float2(a, b);
+  }
+}
+
+template <typename T, int BM, int BN, bool DMA>
+__global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   constexpr int ES = sizeof(T);
   constexpr int BK = 128 / ES;  // elements per K tile
   constexpr int CE = 16 / ES;   // elements per 16-byte chunk
@@ -43,78 +258,92 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs p) {
   constexpr int BI = BN / 32;
   constexpr int FM = BM / 32;   // 16x16 fragments per wave along M (wave tile = BM/2)
   constexpr int FN = BN / 32;
-  __shared__ uint4 smem[2 * (BM + BN) * 8];
+  constexpr int SMEM_MAIN = 2 * (BM + BN) * 8;           // uint4
+  constexpr int PITCH = BN + 4;                          // staged fp32 row pitch
+  constexpr int SMEM_EPI = (BM * PITCH + 3) / 4;         // uint4
+  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  __shared__ uint4 smem[SMEM];
+
+  // ---- tile / split assignment; XCD-aware: blocks b and b+8 share an XCD, give each XCD a
+  //      contiguous run of tile ids so the N tiles of one M panel reuse it from one L2.
+  int tile;
+  {
+    const int bid = blockIdx.x, nblk = p.nblk;
+    const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
+    tile = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+  }
+  const int split = tile % p.ksplit;
+  tile /= p.ksplit;
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk_all = p.kpad / BK;
+  const int kt0 = (int)((int64_t)nk_all * split / p.ksplit);
+  const int kt1 = (int)((int64_t)nk_all * (split + 1) / p.ksplit);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM;
   const int cc = tid & 7, rr = tid >> 3;
 
-  int a_b[AI], a_y[AI], a_x[AI];
-  bool a_ok[AI];
+  const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)p.a0, 0, p.a0_bytes, kBufFlags);
+  const __amdgpu_buffer_rsrc_t ra1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.a1 ? p.a1 : p.a0), 0, p.a1 ? p.a1_bytes : 0, kBufFlags);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, p.w_bytes, kBufFlags);
+
+  // ---- per-row (output pixel) coordinates, fixed for the whole K loop
+  int pix0[AI], iy0[AI], ix0[AI];
+  bool rok[AI];
 #pragma unroll
   for (int i = 0; i < AI; ++i) {
     const int m = m0 + rr + 32 * i;
-    a_ok[i] = m < p.M;
+    rok[i] = m < p.M;
     const int b = m / p.hw_out;
     const int pix = m - b * p.hw_out;
-    a_b[i] = b;
-    a_y[i] = pix / p.w_out;
-    a_x[i] = pix - a_y[i] * p.w_out;
+    const int oy = pix / p.w_out, ox = pix - oy * p.w_out;
+    if (p.upsample) {           // coordinates in the 2x upsampled input
+      iy0[i] = oy - p.pad;
+      ix0[i] = ox - p.pad;
+      pix0[i] = b * p.h_in;
+    } else {
+      iy0[i] = oy * p.stride - p.pad;
+      ix0[i] = ox * p.stride - p.pad;
+      pix0[i] = (b * p.h_in + iy0[i]) * p.w_in + ix0[i];
+    }
   }
+  // ---- this thread's (tap, channel) at the first K tile; advanced incrementally afterwards.
+  //      DMA path: LDS is filled lane-linearly (16 B per lane = 8 rows x 8 chunk positions per
+  //      wave instruction), so the XOR swizzle moves to the SOURCE: the lane at chunk position cc
+  //      of row r fetches logical chunk cc ^ swz(r) (swizzle source + read, never the LDS dest).
+  const int cl = DMA ? (cc ^ ((rr >> 1) & 7)) : cc;
+  int ch = kt0 * BK + cl * CE, tap = ch / p.cin;
+  ch -= tap * p.cin;
+  int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+  const int ntaps = p.ksize * p.ksize;
 
-  uint4 ra[AI], rb[BI];
-  const uint4 zero4 = make_uint4(0, 0, 0, 0);
-
-  auto load_tile = [&](int kt) {
-    const int k = kt * BK + cc * CE;
-    const bool kval = k < p.K;
-    const int tap = k / p.cin;
-    const int ch = k - tap * p.cin;
-    const int ky = tap / p.ksize;
-    const int kx = tap - ky * p.ksize;
-    const char* src;
-    int cs, choff;
-    if (ch < p.c0) { src = p.a0; cs = p.c0; choff = ch; }
-    else { src = p.a1; cs = p.c1; choff = ch - p.c0; }
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      bool ok = a_ok[i] && kval;
-      int iy, ix;
-      if (p.upsample) {
-        const int uy = a_y[i] + ky - p.pad, ux = a_x[i] + kx - p.pad;
-        ok = ok && uy >= 0 && uy < 2 * p.h_in && ux >= 0 && ux < 2 * p.w_in;
-        iy = uy >> 1;
-        ix = ux >> 1;
-      } else {
-        iy = a_y[i] * p.stride + ky - p.pad;
-        ix = a_x[i] * p.stride + kx - p.pad;
-        ok = ok && iy >= 0 && iy < p.h_in && ix >= 0 && ix < p.w_in;
-      }
-      const int64_t off = ((((int64_t)a_b[i] * p.h_in + iy) * p.w_in + ix) * cs + choff) * ES;
-      ra[i] = ok ? *reinterpret_cast<const uint4*>(src + off) : zero4;
+  auto a_offset = [&](int i, int cs, int choff, bool kval) -> int {
+    int pixel;
+    bool ok = rok[i] && kval;
+    if (p.upsample) {
+      const int uy = iy0[i] + ky, ux = ix0[i] + kx;
+      ok = ok && (unsigned)uy < (unsigned)(2 * p.h_in) && (unsigned)ux < (unsigned)(2 * p.w_in);
+      pixel = (pix0[i] + (uy >> 1)) * p.w_in + (ux >> 1);
+    } else {
+      const int iy = iy0[i] + ky, ix = ix0[i] + kx;
+      ok = ok && (unsigned)iy < (unsigned)p.h_in && (unsigned)ix < (unsigned)p.w_in;
+      pixel = pix0[i] + ky * p.w_in + kx;
     }
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const int n = n0 + rr + 32 * i;
-      const int64_t off = ((int64_t)n * p.kpad + kt * BK + cc * CE) * ES;
-      rb[i] = (n < p.n) ? *reinterpret_cast<const uint4*>(p.w + off) : zero4;
-    }
+    return ok ? (pixel * cs + choff) * ES : kOOB;
   };
-
-  auto store_tile = [&](int buf) {
-    uint4* As = smem + buf * (BM + BN) * 8;
-    uint4* Bs = As + BM * 8;
-#pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const int r = rr + 32 * i;
-      As[r * 8 + swz(r, cc)] = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const int r = rr + 32 * i;
-      Bs[r * 8 + swz(r, cc)] = rb[i];
+  auto b_offset = [&](int i, int kt) -> int {
+    const int n = n0 + rr + 32 * i;
+    return (n < p.n) ? (n * p.kpad + kt * BK + cl * CE) * ES : kOOB;
+  };
+  auto advance = [&]() {
+    ch += BK;
+    while (ch >= p.cin) {
+      ch -= p.cin;
+      ++tap;
+      if (++kx == p.ksize) { kx = 0; ++ky; }
     }
   };
 
@@ -128,7 +357,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs p) {
   auto compute = [&](int buf) {
     const uint4* As = smem + buf * (BM + BN) * 8;
     const uint4* Bs = As + BM * 8;
-    constexpr int KSTEPS = (ES == 2) ? 2 : 1;  // 32-wide k steps per tile
+    constexpr int KSTEPS = (ES == 2) ? 2 : 1;
 #pragma unroll
     for (int ks = 0; ks < KSTEPS; ++ks) {
       Frag8<T> af[FM], bfr[FN];
@@ -152,97 +381,184 @@ __global__ __launch_bounds__(256) void igemm_kernel(const ConvArgs p) {
           reinterpret_cast<Frag8<float>&>(bfr[j]).v[1] = Bs[r * 8 + swz(r, 2 * g + 1)];
         }
       }
+      // D[n][m] = W . A^T: lane (g, lr) ends up with channels n = 4g..4g+3 of pixel m = lr
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) mma_k32(acc[i][j], af[i], bfr[j]);
+        for (int j = 0; j < FN; ++j) mma_k32(acc[i][j], bfr[j], af[i]);
     }
   };
 
-  const int nk = p.kpad / BK;
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool more = kt + 1 < nk;
-    if (more) load_tile(kt + 1);
-    compute(kt & 1);
-    if (more) store_tile((kt + 1) & 1);
+  if constexpr (DMA) {
+    // ---- LDS-DMA pipeline: buffer_load_dwordx4 ... lds writes the tile straight into LDS
+    //      (no VGPR staging, no ds_write); out-of-range offsets land as zeros.
+    typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+    const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;   // LDS byte address of smem
+    const int wv = __builtin_amdgcn_readfirstlane(wave);
+    auto issue_dma = [&](int kt, int buf) {
+      const unsigned abase = lds0 + (unsigned)(buf * (BM + BN) * 8 * 16);
+      const unsigned bbase = abase + BM * 8 * 16;
+      const bool kval = tap < ntaps;
+      const int sel = __builtin_amdgcn_readfirstlane((p.c1 > 0 && ch >= p.c0) ? 1 : 0);
+      const int cs = sel ? p.c1 : p.c0;
+      const int choff = sel ? ch - p.c0 : ch;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int off = a_offset(i, cs, choff, kval);
+        const unsigned dst = __builtin_amdgcn_readfirstlane(abase + (32 * i + 8 * wv) * 128);
+        if (sel) dma16(ra1, off, dst);
+        else dma16(ra0, off, dst);
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        const unsigned dst = __builtin_amdgcn_readfirstlane(bbase + (32 * i + 8 * wv) * 128);
+        dma16(rw, b_offset(i, kt), dst);
+      }
+      advance();
+    };
+    if (kt0 < kt1) issue_dma(kt0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int buf = (kt - kt0) & 1;
+      if (kt + 1 < kt1) issue_dma(kt + 1, buf ^ 1);
+      compute(buf);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // ---- register-staged pipeline (per-lane source select for an unaligned concat)
+    uint4 va[AI], vb[BI];
+    auto issue_loads = [&](int kt) {
+      const bool kval = tap < ntaps;
+      const bool lane_src1 = p.c1 > 0 && ch >= p.c0;
+      const int cs = lane_src1 ? p.c1 : p.c0;
+      const int choff = lane_src1 ? ch - p.c0 : ch;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int off = a_offset(i, cs, choff, kval);
+        // the unselected source's load is out of range and reads 0
+        const uint4 x0 = bload(ra0, lane_src1 ? kOOB : off);
+        const uint4 x1 = bload(ra1, lane_src1 ? off : kOOB);
+        va[i] = make_uint4(x0.x | x1.x, x0.y | x1.y, x0.z | x1.z, x0.w | x1.w);
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) vb[i] = bload(rw, b_offset(i, kt));
+      advance();
+    };
+    auto store_lds = [&](int buf) {
+      uint4* As = smem + buf * (BM + BN) * 8;
+      uint4* Bs = As + BM * 8;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int r = rr + 32 * i;
+        As[r * 8 + swz(r, cc)] = va[i];
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        const int r = rr + 32 * i;
+        Bs[r * 8 + swz(r, cc)] = vb[i];
+      }
+    };
+    if (kt0 < kt1) {
+      issue_loads(kt0);
+      store_lds(0);
+    }
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int buf = (kt - kt0) & 1;
+      if (kt + 1 < kt1) issue_loads(kt + 1);
+      compute(buf);
+      if (kt + 1 < kt1) store_lds(buf ^ 1);
+      __syncthreads();
+    }
   }
 
-  // ------------------------------------------------------------------ epilogue
-  const int N = p.n;
-  if (p.out_layout == LDM_OUT_GEGLU) {
-    // columns are packed in 16-wide (hidden, gate) pairs: fragment j even = hidden, j+1 = gate
-    const int nout = N >> 1;
+  // ------------------------------------------------------------------ split-K: raw partials
+  if (p.ksplit > 1) {
+    float* part = p.partial + (int64_t)split * p.M * p.n;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * (BM / 2) + i * 16 + lr;
+      if (m >= p.M) continue;
 #pragma unroll
-      for (int j = 0; j < FN; j += 2) {
-        const int np = n0 + wn * (BN / 2) + j * 16;  // packed column of this pair (multiple of 32)
-        const int nh = np + lr, ng = np + 16 + lr;
-        const int nc = (np >> 1) + lr;
-        if (nh >= N) continue;
-        const float bh = p.bias ? p.bias[nh] : 0.f;
-        const float bg = p.bias ? p.bias[ng] : 0.f;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * (BM / 2) + i * 16 + g * 4 + r;
-          if (m >= p.M) continue;
-          const float h = acc[i][j][r] + bh;
-          const float gt = acc[i][j + 1][r] + bg;
-          const float v = h * gelu_f(gt);
-          const int64_t idx = (int64_t)m * nout + nc;
-          if (p.out_f32) reinterpret_cast<float*>(p.out)[idx] = v;
-          else Elem<T>::store(reinterpret_cast<T*>(p.out) + idx, v);
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * (BN / 2) + j * 16 + 4 * g;
+        if (n >= p.n) continue;
+        float* dst = part + (int64_t)m * p.n + n;
+        if (n + 3 < p.n) {
+          *reinterpret_cast<float4*>(dst) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        } else {
+          for (int r = 0; r < 4 && n + r < p.n; ++r) dst[r] = acc[i][j][r];
         }
       }
     }
     return;
   }
+
+  // ------------------------------------------------------------------ fused epilogue
+  // phase 1: raw accumulators -> LDS [BM][PITCH] fp32
+  float* stage = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
+    const int ml = wm * (BM / 2) + i * 16 + lr;
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * (BN / 2) + j * 16 + lr;
-      if (n >= N) continue;
-      const float bn = p.bias ? p.bias[n] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * (BM / 2) + i * 16 + g * 4 + r;
-        if (m >= p.M) continue;
-        const int b = m / p.hw_out;
-        float v = acc[i][j][r] + bn;
-        if (p.temb) v += p.temb[(int64_t)b * p.temb_stride + n];
-        if (p.act == LDM_ACT_SILU) v = silu_f(v);
-        int64_t idx;
-        if (p.out_layout == LDM_OUT_NHWC) {
-          idx = (int64_t)m * N + n;
-        } else if (p.out_layout == LDM_OUT_NCHW) {
-          const int pix = m - b * p.hw_out;
-          idx = ((int64_t)b * N + n) * p.hw_out + pix;
-        } else {  // LDM_OUT_SHUFFLE2: n = (dy*2+dx)*Cout + co -> pixel (2y+dy, 2x+dx)
-          const int cout = N >> 2;
-          const int q = n / cout, co = n - q * cout;
-          const int dy = q >> 1, dx = q & 1;
-          const int pix = m - b * p.hw_out;
-          const int y = pix / p.w_out, x = pix - y * p.w_out;
-          idx = (((int64_t)b * 2 * p.h_out + 2 * y + dy) * 2 * p.w_out + 2 * x + dx) * cout + co;
-        }
-        if (p.residual) v += to_f(reinterpret_cast<const T*>(p.residual)[idx]);
-        if (p.out_f32) reinterpret_cast<float*>(p.out)[idx] = v;
-        else Elem<T>::store(reinterpret_cast<T*>(p.out) + idx, v);
-      }
+      const int nl = wn * (BN / 2) + j * 16 + 4 * g;
+      *reinterpret_cast<float4*>(stage + ml * PITCH + nl) =
+          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
     }
   }
+  __syncthreads();
+  // phase 2: coalesced rows; the statistics reduction reuses the space past the stage
+  float* red = stage;  // overwritten only after every thread has read its stage values
+  auto raw = [&](int r, int c4, float* v) {
+    const float4 x = *reinterpret_cast<const float4*>(stage + r * PITCH + 4 * c4);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  };
+  epilogue_rows<T, BM, BN>(p, m0, n0, raw, red);
+}
+
+// Split-K reduction + full epilogue: one block per 64-row x 128-channel tile.
+template <typename T>
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) {
+  __shared__ float red[(256 / 32) * 32 * 1 * 4 * 2];
+  const int tiles_n = (p.n + 127) / 128;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
+  const int m0 = tm * 64, n0 = tn * 128;
+  const int64_t slab = (int64_t)p.M * p.n;
+  auto raw = [&](int r, int c4, float* v) {
+    const int m = m0 + r, n = n0 + 4 * c4;
+    const float* src = p.partial + (int64_t)m * p.n + n;
+    v[0] = v[1] = v[2] = v[3] = 0.f;
+    if (n + 3 < p.n) {
+      for (int s = 0; s < p.ksplit; ++s) {
+        const float4 x = *reinterpret_cast<const float4*>(src + s * slab);
+        v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
+      }
+    } else {
+      for (int s = 0; s < p.ksplit; ++s)
+        for (int r2 = 0; r2 < 4 && n + r2 < p.n; ++r2) v[r2] += src[s * slab + r2];
+    }
+  };
+  epilogue_rows<T, 64, 128>(p, m0, n0, raw, red);
 }
 
 template <typename T, int BM, int BN>
-int launch_bm_bn(const ConvArgs& a, hipStream_t s) {
-  dim3 grid((a.n + BN - 1) / BN, (a.M + BM - 1) / BM);
-  hipLaunchKernelGGL((igemm_kernel<T, BM, BN>), grid, dim3(256), 0, s, a);
+int launch_bm_bn(ConvArgs a, hipStream_t s) {
+  a.tiles_n = (a.n + BN - 1) / BN;
+  const int tiles_m = (a.M + BM - 1) / BM;
+  a.nblk = tiles_m * a.tiles_n * a.ksplit;
+  if (a.mixed_src)
+    hipLaunchKernelGGL((igemm_kernel<T, BM, BN, false>), dim3(a.nblk), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((igemm_kernel<T, BM, BN, true>), dim3(a.nblk), dim3(256), 0, s, a);
   LDM_CHECK_LAUNCH();
+  if (a.ksplit > 1) {
+    const int blocks = ((a.M + 63) / 64) * ((a.n + 127) / 128);
+    hipLaunchKernelGGL((splitk_epilogue_kernel<T>), dim3(blocks), dim3(256), 0, s, a);
+    LDM_CHECK_LAUNCH();
+  }
   return LDM_OK;
 }
 
@@ -262,9 +578,31 @@ int launch_t(const ConvArgs& a, hipStream_t s, int bm, int bn) {
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-}  // namespace
+struct Plan {
+  int bm, bn, ksplit;
+};
 
-extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
+Plan make_plan(const ldm_conv_params* q, int M, int es) {
+  Plan pl;
+  pl.bm = M <= 32 ? 32 : (M <= 64 ? 64 : 128);
+  pl.bn = q->n <= 32 ? 32 : (q->n <= 64 ? 64 : 128);
+  if (q->out_layout == LDM_OUT_GEGLU && pl.bn < 64) pl.bn = 64;
+  pl.ksplit = 1;
+  // Split K when the tile grid cannot fill the chip (the 8x8 / 16x16 UNet levels): aim for
+  // ~2 blocks per CU, keep >= 8 K tiles per split.  Not for GEGLU / pixel-shuffle outputs.
+  const int bk = 128 / es;
+  const int nk = q->kpad / bk;
+  const int tiles = ((M + pl.bm - 1) / pl.bm) * ((q->n + pl.bn - 1) / pl.bn);
+  if (q->out_layout != LDM_OUT_GEGLU && q->out_layout != LDM_OUT_SHUFFLE2 && tiles < 256 && nk >= 16) {
+    int ks = (512 + tiles - 1) / tiles;
+    ks = std::min(ks, nk / 8);
+    ks = std::min(ks, 16);
+    if (ks > 1) pl.ksplit = ks;
+  }
+  return pl;
+}
+
+int validate(const ldm_conv_params* q, int* es_out) {
   if (!q) return LDM_ERR_ARG;
   if (q->dtype != LDM_F32 && q->dtype != LDM_BF16) return LDM_ERR_ARG;
   const int es = q->dtype == LDM_F32 ? 4 : 2;
@@ -277,37 +615,74 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   if (q->c0 % ce || q->c1 % ce) return LDM_ERR_ALIGN;
   if (q->kpad % 64) return LDM_ERR_ALIGN;
   const int cin = q->c0 + q->c1;
-  const int K = q->ksize * q->ksize * cin;
-  if (K > q->kpad || q->n <= 0) return LDM_ERR_ARG;
+  if (q->ksize * q->ksize * cin > q->kpad || q->n <= 0) return LDM_ERR_ARG;
   if (!aligned16(q->a0) || (q->a1 && !aligned16(q->a1)) || !aligned16(q->w)) return LDM_ERR_ALIGN;
   const int pad = q->ksize / 2;
   const int hin_eff = q->upsample ? 2 * q->h_in : q->h_in;
   const int win_eff = q->upsample ? 2 * q->w_in : q->w_in;
   if (q->h_out != (hin_eff + 2 * pad - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
   if (q->w_out != (win_eff + 2 * pad - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
-  if (q->out_layout == LDM_OUT_GEGLU && (q->n % 32 || q->residual || q->temb)) return LDM_ERR_ARG;
-  if (q->out_layout == LDM_OUT_SHUFFLE2 && (q->n % 4 || q->temb || q->upsample)) return LDM_ERR_ARG;
+  if (q->out_layout == LDM_OUT_GEGLU && (q->n % 32 || q->residual || q->temb || q->gn_partial)) return LDM_ERR_ARG;
+  if (q->out_layout == LDM_OUT_SHUFFLE2 && (q->n % 16 || q->temb || q->upsample)) return LDM_ERR_ARG;
+  if (q->out_layout < 0 || q->out_layout > 3) return LDM_ERR_ARG;
   const int64_t M64 = (int64_t)q->batch * q->h_out * q->w_out;
-  if (M64 >= (1LL << 31)) return LDM_ERR_ARG;
+  if (q->gn_partial && (M64 % 64 || (q->h_out * q->w_out) % 64 || q->out_layout != LDM_OUT_NHWC)) return LDM_ERR_ARG;
+  const int64_t a0_bytes = (int64_t)q->batch * q->h_in * q->w_in * q->c0 * es;
+  const int64_t a1_bytes = (int64_t)q->batch * q->h_in * q->w_in * q->c1 * es;
+  const int64_t w_bytes = (int64_t)q->n * q->kpad * es;
+  if (M64 >= (1LL << 31) || a0_bytes >= (1LL << 31) - 64 || a1_bytes >= (1LL << 31) - 64 ||
+      w_bytes >= (1LL << 31) - 64)
+    return LDM_ERR_ARG;  // 32-bit buffer offsets
+  *es_out = es;
+  return LDM_OK;
+}
+
+}  // namespace
+
+extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
+  int es = 0;
+  if (validate(q, &es) != LDM_OK) return 0;
+  const int M = q->batch * q->h_out * q->w_out;
+  const Plan pl = make_plan(q, M, es);
+  return pl.ksplit > 1 ? (size_t)pl.ksplit * M * q->n * sizeof(float) : 0;
+}
+
+extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
+  int es = 0;
+  const int st = validate(q, &es);
+  if (st != LDM_OK) return st;
+  const int bk = 128 / es;
+  const int cin = q->c0 + q->c1;
+  const int M = q->batch * q->h_out * q->w_out;
+  const Plan pl = make_plan(q, M, es);
+  if (pl.ksplit > 1) {
+    const size_t need = (size_t)pl.ksplit * M * q->n * sizeof(float);
+    if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;
+  }
 
   ConvArgs a;
   a.a0 = static_cast<const char*>(q->a0);
   a.a1 = static_cast<const char*>(q->a1);
+  a.a0_bytes = (int)((int64_t)q->batch * q->h_in * q->w_in * q->c0 * es);
+  a.a1_bytes = (int)((int64_t)q->batch * q->h_in * q->w_in * q->c1 * es);
   a.c0 = q->c0; a.c1 = q->c1; a.cin = cin;
-  a.batch = q->batch; a.h_in = q->h_in; a.w_in = q->w_in;
+  a.h_in = q->h_in; a.w_in = q->w_in;
   a.h_out = q->h_out; a.w_out = q->w_out; a.hw_out = q->h_out * q->w_out;
-  a.ksize = q->ksize; a.stride = q->stride; a.upsample = q->upsample; a.pad = pad;
+  a.ksize = q->ksize; a.stride = q->stride; a.upsample = q->upsample; a.pad = q->ksize / 2;
   a.w = static_cast<const char*>(q->w);
-  a.n = q->n; a.kpad = q->kpad; a.K = K;
+  a.w_bytes = (int)((int64_t)q->n * q->kpad * es);
+  a.n = q->n; a.kpad = q->kpad; a.K = q->ksize * q->ksize * cin;
   a.bias = q->bias; a.temb = q->temb; a.temb_stride = q->temb_stride;
   a.residual = static_cast<const char*>(q->residual);
   a.out = static_cast<char*>(q->out);
   a.out_layout = q->out_layout; a.act = q->act; a.out_f32 = q->out_f32;
-  a.M = (int)M64;
-
-  const int bm = a.M <= 32 ? 32 : (a.M <= 64 ? 64 : 128);
-  int bn = a.n <= 32 ? 32 : (a.n <= 64 ? 64 : 128);
-  if (q->out_layout == LDM_OUT_GEGLU && bn < 64) bn = 64;
+  a.M = M;
+  a.tiles_n = 0;
+  a.nblk = 0;
+  a.mixed_src = (q->c1 > 0 && (q->c0 % bk || q->c1 % bk)) ? 1 : 0;
+  a.ksplit = pl.ksplit;
+  a.partial = static_cast<float*>(q->workspace);
+  a.gn_part = reinterpret_cast<float2*>(q->gn_partial);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, s, bm, bn) : launch_t<float>(a, s, bm, bn);
+  return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, s, pl.bm, pl.bn) : launch_t<float>(a, s, pl.bm, pl.bn);
 }

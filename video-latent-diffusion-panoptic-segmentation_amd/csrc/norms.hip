@@ -1,23 +1,23 @@
 // GroupNorm(+SiLU) and LayerNorm over NHWC rows (ldm_group_norm / ldm_layer_norm).
 //
-// GroupNorm is HBM-bound: 3 kernels, all 16-B vectorised and coalesced along channels.
-//   gn_partial : per (batch, 64-pixel chunk) per-channel fp32 (sum, sumsq)  -> workspace
-//   gn_finalize: per (batch, group) fp64 reduction of the partials         -> (mean, rstd)
-//   gn_apply   : y = silu?((x - mean) * rstd * gamma + beta)  written as one NHWC tensor
+// GroupNorm is HBM-bound.  Statistics come as per-channel (sum, sumsq) partials over 64-pixel
+// chunks — normally written by the producing conv's epilogue (ldm_conv2d gn_partial), so the
+// tensor is NOT re-read for them; otherwise gn_partial computes them here.
+//   gn_finalize: per (batch, group) fp64 reduction -> per-(batch, channel) scale/shift table
+//   gn_apply   : y = silu?(x * scale + shift), one 16-B vector per thread, one read + one write
 // Inputs may be the channel concatenation of two NHWC tensors (up-block [hidden || skip]),
-// read in place.  Algorithmic traffic: 2 reads + 1 write of the tensor.
+// read in place.
 #include "common.h"
 
 namespace {
 
-constexpr int GN_PPC = 64;  // pixels per partial chunk
+constexpr int GN_PPC = 64;  // pixels per partial chunk (== the conv epilogue's 64-row chunks)
 
 template <typename T>
-__global__ __launch_bounds__(256) void gn_partial(const T* __restrict__ x0, const T* __restrict__ x1,
-                                                  int c0, int c1, int hw, int chunks,
+__global__ __launch_bounds__(256) void gn_partial(const T* __restrict__ x, int C, int hw, int chunks,
                                                   float2* __restrict__ part) {
   constexpr int EPC = 16 / sizeof(T);
-  const int C = c0 + c1, V = C / EPC;
+  const int V = C / EPC;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int v = blockIdx.x * 64 + tx;
   const int chunk = blockIdx.y, b = blockIdx.z;
@@ -25,13 +25,9 @@ __global__ __launch_bounds__(256) void gn_partial(const T* __restrict__ x0, cons
 #pragma unroll
   for (int e = 0; e < EPC; ++e) { s[e] = 0.f; ss[e] = 0.f; }
   if (v < V) {
-    const int c = v * EPC;
-    const T* src;
-    int cs, co;
-    if (c < c0) { src = x0; cs = c0; co = c; } else { src = x1; cs = c1; co = c - c0; }
     const int p0 = chunk * GN_PPC, p1 = min(hw, p0 + GN_PPC);
     for (int pix = p0 + ty; pix < p1; pix += 4) {
-      const uint4 raw = *reinterpret_cast<const uint4*>(src + ((int64_t)b * hw + pix) * cs + co);
+      const uint4 raw = *reinterpret_cast<const uint4*>(x + ((int64_t)b * hw + pix) * C + v * EPC);
       const T* e = reinterpret_cast<const T*>(&raw);
 #pragma unroll
       for (int k = 0; k < EPC; ++k) {
@@ -56,39 +52,45 @@ __global__ __launch_bounds__(256) void gn_partial(const T* __restrict__ x0, cons
   }
 }
 
-__global__ __launch_bounds__(256) void gn_finalize(const float2* __restrict__ part, int C, int hw, int chunks,
-                                                   int groups, float eps, float2* __restrict__ stats) {
+// one wave per (batch, group): fp64 sum of the partials, then the group's scale/shift entries
+__global__ __launch_bounds__(256) void gn_finalize(const float2* __restrict__ part0, const float2* __restrict__ part1,
+                                                   int c0, int c1, int hw, int chunks, int groups, float eps,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   float2* __restrict__ table) {
   const int b = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int cpg = C / groups;
+  const int gi = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (gi >= groups) return;
+  const int C = c0 + c1, cpg = C / groups;
   const int n = chunks * cpg;
-  for (int gi = wave; gi < groups; gi += 4) {
-    double a = 0.0, q = 0.0;
-    for (int i = lane; i < n; i += 64) {
-      const int ch = i / cpg, cc = i - ch * cpg;
-      const float2 v = part[((int64_t)b * chunks + ch) * C + gi * cpg + cc];
-      a += v.x;
-      q += v.y;
-    }
+  double a = 0.0, q = 0.0;
+  for (int i = lane; i < n; i += 64) {
+    const int ch = i / cpg, c = gi * cpg + (i - ch * cpg);
+    const int64_t row = (int64_t)b * chunks + ch;
+    const float2 v = c < c0 ? part0[row * c0 + c] : part1[row * c1 + (c - c0)];
+    a += v.x;
+    q += v.y;
+  }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); q += __shfl_xor(q, o, 64); }
-    if (lane == 0) {
-      const double cnt = (double)hw * cpg;
-      const double mean = a / cnt;
-      double var = q / cnt - mean * mean;
-      if (var < 0.0) var = 0.0;
-      stats[b * groups + gi] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
-    }
+  for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); q += __shfl_xor(q, o, 64); }
+  const double cnt = (double)hw * cpg;
+  const double mean = a / cnt;
+  double var = q / cnt - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  for (int k = lane; k < cpg; k += 64) {
+    const int c = gi * cpg + k;
+    const float sc = rstd * gamma[c];
+    table[(int64_t)b * C + c] = make_float2(sc, beta[c] - (float)mean * sc);
   }
 }
 
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x0, const T* __restrict__ x1, int c0, int c1,
-                                                int hw, int64_t nvec, int groups, const float2* __restrict__ stats,
-                                                const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                int act, T* __restrict__ out) {
+                                                int hw, int64_t nvec, const float2* __restrict__ table, int act,
+                                                T* __restrict__ out) {
   constexpr int EPC = 16 / sizeof(T);
-  const int C = c0 + c1, V = C / EPC, cpg = C / groups;
+  const int C = c0 + c1, V = C / EPC;
   for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
     const int64_t m = i / V;
     const int v = (int)(i - m * V);
@@ -97,15 +99,17 @@ __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x0, const 
     const uint4 raw = (c < c0) ? *reinterpret_cast<const uint4*>(x0 + m * c0 + c)
                                : *reinterpret_cast<const uint4*>(x1 + m * c1 + (c - c0));
     const T* e = reinterpret_cast<const T*>(&raw);
+    const float4* tb = reinterpret_cast<const float4*>(table + (int64_t)b * C + c);
     uint4 res;
     T* r = reinterpret_cast<T*>(&res);
 #pragma unroll
-    for (int k = 0; k < EPC; ++k) {
-      const int ch = c + k;
-      const float2 st = stats[b * groups + ch / cpg];
-      float y = (to_f(e[k]) - st.x) * st.y * gamma[ch] + beta[ch];
-      if (act == LDM_ACT_SILU) y = silu_f(y);
-      r[k] = from_f<T>(y);
+    for (int k = 0; k < EPC; k += 2) {
+      const float4 st = tb[k >> 1];   // (scale_k, shift_k, scale_k+1, shift_k+1)
+      float y0 = to_f(e[k]) * st.x + st.y;
+      float y1 = to_f(e[k + 1]) * st.z + st.w;
+      if (act == LDM_ACT_SILU) { y0 = silu_f(y0); y1 = silu_f(y1); }
+      r[k] = from_f<T>(y0);
+      r[k + 1] = from_f<T>(y1);
     }
     *reinterpret_cast<uint4*>(out + m * C + c) = res;
   }
@@ -164,26 +168,42 @@ __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, int ro
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+inline size_t round16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 template <typename T>
 int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups, const float* gamma,
-              const float* beta, float eps, int act, void* out, void* ws, hipStream_t s) {
+              const float* beta, float eps, int act, void* out, const float* p0, const float* p1, void* ws,
+              hipStream_t s) {
   constexpr int EPC = 16 / sizeof(T);
   const int C = c0 + c1;
-  const int V = C / EPC;
   const int chunks = (hw + GN_PPC - 1) / GN_PPC;
-  float2* part = static_cast<float2*>(ws);
-  float2* stats = part + (size_t)batch * chunks * C;
-  hipLaunchKernelGGL((gn_partial<T>), dim3((V + 63) / 64, chunks, batch), dim3(256), 0, s,
-                     static_cast<const T*>(x0), static_cast<const T*>(x1), c0, c1, hw, chunks, part);
+  char* w = static_cast<char*>(ws);
+  float2* table = reinterpret_cast<float2*>(w);
+  w += round16((size_t)batch * C * sizeof(float2));
+  const float2* part0 = reinterpret_cast<const float2*>(p0);
+  const float2* part1 = reinterpret_cast<const float2*>(p1);
+  if (!part0) {
+    float2* dst = reinterpret_cast<float2*>(w);
+    w += round16((size_t)batch * chunks * c0 * sizeof(float2));
+    hipLaunchKernelGGL((gn_partial<T>), dim3((c0 / EPC + 63) / 64, chunks, batch), dim3(256), 0, s,
+                       static_cast<const T*>(x0), c0, hw, chunks, dst);
+    LDM_CHECK_LAUNCH();
+    part0 = dst;
+  }
+  if (c1 > 0 && !part1) {
+    float2* dst = reinterpret_cast<float2*>(w);
+    hipLaunchKernelGGL((gn_partial<T>), dim3((c1 / EPC + 63) / 64, chunks, batch), dim3(256), 0, s,
+                       static_cast<const T*>(x1), c1, hw, chunks, dst);
+    LDM_CHECK_LAUNCH();
+    part1 = dst;
+  }
+  hipLaunchKernelGGL(gn_finalize, dim3(batch, (groups + 3) / 4), dim3(256), 0, s, part0, part1, c0, c1, hw, chunks,
+                     groups, eps, gamma, beta, table);
   LDM_CHECK_LAUNCH();
-  hipLaunchKernelGGL(gn_finalize, dim3(batch), dim3(256), 0, s, part, C, hw, chunks, groups, eps, stats);
-  LDM_CHECK_LAUNCH();
-  const int64_t nvec = (int64_t)batch * hw * V;
-  const int64_t blocks = std::min<int64_t>((nvec + 255) / 256, 256 * 16);
+  const int64_t nvec = (int64_t)batch * hw * (C / EPC);
+  const int64_t blocks = std::min<int64_t>((nvec + 255) / 256, 256 * 8);
   hipLaunchKernelGGL((gn_apply<T>), dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const T*>(x0),
-                     static_cast<const T*>(x1), c0, c1, hw, nvec, groups, stats, gamma, beta, act,
-                     static_cast<T*>(out));
+                     static_cast<const T*>(x1), c0, c1, hw, nvec, table, act, static_cast<T*>(out));
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
@@ -192,24 +212,29 @@ int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw,
 
 extern "C" size_t ldm_group_norm_workspace_bytes(int batch, int hw, int channels) {
   const size_t chunks = (hw + GN_PPC - 1) / GN_PPC;
-  return (size_t)batch * chunks * channels * sizeof(float2) + (size_t)batch * 512 * sizeof(float2) + 256;
+  return round16((size_t)batch * channels * sizeof(float2)) + 2 * round16((size_t)batch * chunks * channels *
+                                                                          sizeof(float2)) + 64;
 }
 
 extern "C" int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
-                              const float* gamma, const float* beta, float eps, int act, void* out, void* workspace,
-                              int dtype, ldm_stream_t stream) {
+                              const float* gamma, const float* beta, float eps, int act, void* out,
+                              const float* stats0, const float* stats1, void* workspace, int dtype,
+                              ldm_stream_t stream) {
   if (!x0 || !out || !workspace || !gamma || !beta) return LDM_ERR_ARG;
   if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
-  if (batch <= 0 || hw <= 0 || c0 <= 0 || c1 < 0 || (c1 > 0 && !x1) || groups <= 0 || groups > 512) return LDM_ERR_ARG;
+  if (batch <= 0 || hw <= 0 || c0 <= 0 || c1 < 0 || (c1 > 0 && !x1) || groups <= 0) return LDM_ERR_ARG;
   const int C = c0 + c1;
   if (C % groups) return LDM_ERR_ARG;
+  if ((stats0 || stats1) && hw % GN_PPC) return LDM_ERR_ARG;   // producer partials use 64-row chunks
   const int epc = dtype == LDM_F32 ? 4 : 8;
   if (c0 % epc || c1 % epc) return LDM_ERR_ALIGN;
   if (!aligned16(x0) || (x1 && !aligned16(x1)) || !aligned16(out) || !aligned16(workspace)) return LDM_ERR_ALIGN;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (dtype == LDM_BF16)
-    return gn_launch<bf16_t>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, workspace, s);
-  return gn_launch<float>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, workspace, s);
+    return gn_launch<bf16_t>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1,
+                             workspace, s);
+  return gn_launch<float>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1, workspace,
+                          s);
 }
 
 extern "C" int ldm_layer_norm(const void* x, int rows, int c, const float* gamma, const float* beta, float eps,

@@ -416,14 +416,14 @@ class UNet(nn.Module):
         p = P[id(r)]
         x0, x1 = xs
         h = K.group_norm(x0, B, H * W, r.groups, *p["n1"], r.eps, K.ACT_SILU, x1=x1)
-        h = K.conv2d(p["c1"], h, B, H, W, temb=temb_all[:, p["off"]:], temb_stride=temb_all.shape[1])
+        h = K.conv2d(p["c1"], h, B, H, W, temb=temb_all[:, p["off"]:], temb_stride=temb_all.shape[1], gn_stats=True)
         h = K.group_norm(h, B, H * W, r.groups, *p["n2"], r.eps, K.ACT_SILU)
         if p["sc"] is not None:
             res = K.conv2d(p["sc"], x0, B, H, W, x1=x1)
         else:
             assert x1 is None
             res = x0
-        return K.conv2d(p["c2"], h, B, H, W, residual=res)
+        return K.conv2d(p["c2"], h, B, H, W, residual=res, gn_stats=True)
 
     def _transformer(self, P, t, x, B, H, W, ehs):
         p = P[id(t)]
@@ -448,7 +448,7 @@ class UNet(nn.Module):
         n = K.layer_norm(h, *p["ln3"], 1e-5)
         f = K.linear(p["ff1"], n, out_layout=K.OUT_GEGLU)                # [B, N, 4C]
         h = K.linear(p["ff2"], f, residual=h, out=h)
-        return K.linear(p["proj_out"], h, residual=x)
+        return K.conv2d(p["proj_out"], h, B, H, W, residual=x, gn_stats=True)
 
     @torch.no_grad()
     def forward(
@@ -498,7 +498,7 @@ class UNet(nn.Module):
         temb_all = K.linear(P["temb_proj"], emb, out_dtype=torch.float32)  # [B, sum Cout]
         # 3. conv_in (unet.py:357)
         x = K.nchw_to_nhwc(sources, P["cin_pad"], dt)
-        x = K.conv2d(P["conv_in"], x, B, H, W)
+        x = K.conv2d(P["conv_in"], x, B, H, W, gn_stats=True)
         skips = [(x, H, W)]
         for blk in self.down_blocks:
             for j, r in enumerate(blk.resnets):
@@ -507,7 +507,7 @@ class UNet(nn.Module):
                     x = self._transformer(P, blk.attentions[j], x, B, H, W, encoder_hidden_states)
                 skips.append((x, H, W))
             if blk.downsamplers is not None:
-                x = K.conv2d(P[id(blk.downsamplers[0])], x, B, H, W, stride=2)
+                x = K.conv2d(P[id(blk.downsamplers[0])], x, B, H, W, stride=2, gn_stats=True)
                 H, W = (H + 1) // 2, (W + 1) // 2
                 skips.append((x, H, W))
         mb = self.mid_block
@@ -522,7 +522,7 @@ class UNet(nn.Module):
                 if blk.has_cross_attention:
                     x = self._transformer(P, blk.attentions[j], x, B, H, W, encoder_hidden_states)
             if blk.upsamplers is not None:
-                x = K.conv2d(P[id(blk.upsamplers[0])], x, B, H, W, upsample=True)
+                x = K.conv2d(P[id(blk.upsamplers[0])], x, B, H, W, upsample=True, gn_stats=True)
                 H, W = 2 * H, 2 * W
         x = K.group_norm(x, B, H * W, self.conv_norm_out.num_groups, *P["out_norm"], self.conv_norm_out.eps,
                          K.ACT_SILU)

@@ -31,7 +31,8 @@ class ConvParams(ctypes.Structure):
     _fields_ = [("a0", _vp), ("a1", _vp), ("c0", _i), ("c1", _i), ("batch", _i), ("h_in", _i), ("w_in", _i),
                 ("h_out", _i), ("w_out", _i), ("ksize", _i), ("stride", _i), ("upsample", _i), ("w", _vp),
                 ("n", _i), ("kpad", _i), ("bias", _vp), ("temb", _vp), ("temb_stride", _i), ("residual", _vp),
-                ("out", _vp), ("out_layout", _i), ("act", _i), ("dtype", _i), ("out_f32", _i)]
+                ("out", _vp), ("out_layout", _i), ("act", _i), ("dtype", _i), ("out_f32", _i),
+                ("workspace", _vp), ("workspace_bytes", _i64), ("gn_partial", _vp)]
 
 
 class AttnParams(ctypes.Structure):
@@ -49,9 +50,10 @@ class DdimParams(ctypes.Structure):
 
 EXPORTS = {
     "ldm_conv2d": (_i, [ctypes.POINTER(ConvParams), _vp]),
+    "ldm_conv2d_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(ConvParams)]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_group_norm_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
-    "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _i, _vp]),
+    "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _i, _vp]),
     "ldm_layer_norm": (_i, [_vp, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp]),
     "ldm_timestep_proj": (_i, [_vp, _i, _i, _vp, _i, _i, _vp, _i, _vp]),
     "ldm_ddim_step": (_i, [ctypes.POINTER(DdimParams), _vp]),
@@ -136,16 +138,16 @@ class LaunchProfiler:
         ev.record()
         return ev
 
-    def stop(self, family, flops, nbytes, ev0):
+    def stop(self, family, flops, nbytes, ev0, detail=""):
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record()
-        self.records.append((family, flops, nbytes, ev0, ev1))
+        self.records.append((family, flops, nbytes, ev0, ev1, detail))
 
-    def summary(self):
+    def summary(self, by_detail=False):
         torch.cuda.synchronize()
         fam = {}
-        for f, fl, by, e0, e1 in self.records:
-            d = fam.setdefault(f, dict(launches=0, ms=0.0, flops=0.0, bytes=0.0))
+        for f, fl, by, e0, e1, det in self.records:
+            d = fam.setdefault((f, det) if by_detail else f, dict(launches=0, ms=0.0, flops=0.0, bytes=0.0))
             d["launches"] += 1
             d["ms"] += e0.elapsed_time(e1)
             d["flops"] += fl
@@ -165,9 +167,9 @@ def _prof_start():
     return _PROFILER.start() if _PROFILER is not None else None
 
 
-def _prof_stop(ev0, family, flops, nbytes):
+def _prof_stop(ev0, family, flops, nbytes, detail=""):
     if ev0 is not None:
-        _PROFILER.stop(family, flops, nbytes, ev0)
+        _PROFILER.stop(family, flops, nbytes, ev0, detail)
 
 
 # ======================================================================================
@@ -224,9 +226,20 @@ class PackedConv:
         self.shuffle2 = shuffle2
 
 
+GN_PART_ATTR = "_ldm_gn_part"
+
+
+def gn_stats_of(t):
+    """The (sum, sumsq) partial slab a conv epilogue attached to tensor ``t`` (or None)."""
+    return getattr(t, GN_PART_ATTR, None) if t is not None else None
+
+
 def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False, temb=None, temb_stride=0,
-           residual=None, out=None, out_layout=OUT_NHWC, act=ACT_NONE, out_dtype=None):
-    """Run ldm_conv2d.  x0/x1: NHWC [batch, h, w, c] (any contiguous view with that numel)."""
+           residual=None, out=None, out_layout=OUT_NHWC, act=ACT_NONE, out_dtype=None, gn_stats=False):
+    """Run ldm_conv2d.  x0/x1: NHWC [batch, h, w, c] (any contiguous view with that numel).
+
+    gn_stats=True also has the epilogue write per-64-row-chunk channel (sum, sumsq) of the
+    output; the slab is attached to the returned tensor and consumed by group_norm()."""
     lib = load_library()
     _gpu(x0, x1, pc.w, temb, residual, out)
     c0 = x0.numel() // (batch * h * w)
@@ -268,17 +281,28 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
             raise ValueError("temb must be an fp32 [batch, >=n] row-major view")
         if temb.shape[1] < n or temb.stride(0) != temb_stride:
             raise ValueError("temb view narrower than n or stride mismatch")
+    M = batch * ho * wo
+    part = None
+    if gn_stats and out_layout == OUT_NHWC and M % 64 == 0 and (ho * wo) % 64 == 0:
+        part = torch.empty(M // 64, n, 2, dtype=torch.float32, device=x0.device)
     p = ConvParams(_ptr(x0), _ptr(x1), c0, c1, batch, h, w, ho, wo, pc.ksize, stride, int(upsample), _ptr(pc.w),
                    n, pc.kpad, _ptr(pc.bias), _ptr(temb), temb_stride, _ptr(residual), _ptr(out), out_layout, act,
-                   dtype_code(pc.dtype), int(odt == torch.float32 and pc.dtype != torch.float32))
+                   dtype_code(pc.dtype), int(odt == torch.float32 and pc.dtype != torch.float32), None, 0,
+                   _ptr(part))
+    ws_bytes = int(lib.ldm_conv2d_workspace_bytes(ctypes.byref(p)))
+    if ws_bytes:
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x0.device)
+        p.workspace, p.workspace_bytes = _ptr(ws), ws_bytes
     ev = _prof_start()
     _check(lib.ldm_conv2d(ctypes.byref(p), _stream(x0)), "ldm_conv2d")
+    setattr(out, GN_PART_ATTR, part)     # never leave a stale slab on a rewritten tensor
     if ev is not None:
-        M = batch * ho * wo
         flops = 2.0 * M * n * pc.ksize * pc.ksize * pc.cin_real
         nbytes = (x0.numel() + (0 if x1 is None else x1.numel()) + pc.w.numel()) * x0.element_size() + \
             out.numel() * out.element_size() + (0 if residual is None else residual.numel() * residual.element_size())
-        _prof_stop(ev, "igemm", flops, nbytes)
+        det = f"k{pc.ksize}{'s2' if stride == 2 else ''}{'up' if upsample else ''} M={M} N={n} " \
+              f"Cin={c0}+{c1} L{out_layout}"
+        _prof_stop(ev, "igemm", flops, nbytes, det)
     return out
 
 
@@ -287,8 +311,11 @@ def linear(pc: PackedConv, x, **kw):
     rows = x.numel() // x.shape[-1]
     y = conv2d(pc, x, rows, 1, 1, **kw)
     if kw.get("out_layout", OUT_NHWC) == OUT_GEGLU:
-        return y.view(*x.shape[:-1], pc.n // 2)
-    return y.view(*x.shape[:-1], y.shape[-1])
+        v = y.view(*x.shape[:-1], pc.n // 2)
+    else:
+        v = y.view(*x.shape[:-1], y.shape[-1])
+    setattr(v, GN_PART_ATTR, gn_stats_of(y))
+    return v
 
 
 # ======================================================================================
@@ -311,7 +338,7 @@ def attention(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_
     ev = _prof_start()
     _check(lib.ldm_attention(ctypes.byref(p), _stream(q)), "ldm_attention")
     _prof_stop(ev, "attention", 4.0 * batch * heads * n_q * n_kv * head_dim,
-               (2 * batch * n_q * C + 2 * batch * n_kv * C) * q.element_size())
+               (2 * batch * n_q * C + 2 * batch * n_kv * C) * q.element_size(), f"N={n_q} L={n_kv} d={head_dim}")
     return out
 
 
@@ -329,10 +356,19 @@ def group_norm(x0, batch, hw, groups, gamma, beta, eps, act=ACT_NONE, x1=None, o
     if out is None:
         out = torch.empty(batch, hw, C, dtype=x0.dtype, device=x0.device)
     ws = torch.empty(int(lib.ldm_group_norm_workspace_bytes(batch, hw, C)), dtype=torch.uint8, device=x0.device)
+    s0, s1 = gn_stats_of(x0), gn_stats_of(x1)
+    if hw % 64:
+        s0 = s1 = None
+    for s, c in ((s0, c0), (s1, c1)):
+        if s is not None and s.numel() != (batch * hw // 64) * c * 2:
+            raise ValueError("attached GroupNorm partials do not match the tensor")
     ev = _prof_start()
     _check(lib.ldm_group_norm(_ptr(x0), _ptr(x1), c0, c1, batch, hw, groups, _ptr(gamma), _ptr(beta), float(eps),
-                              act, _ptr(out), _ptr(ws), dtype_code(x0.dtype), _stream(x0)), "ldm_group_norm")
-    _prof_stop(ev, "group_norm", 0.0, 3.0 * out.numel() * out.element_size())
+                              act, _ptr(out), _ptr(s0), _ptr(s1), _ptr(ws), dtype_code(x0.dtype), _stream(x0)),
+           "ldm_group_norm")
+    passes = 2.0 + (s0 is None) * c0 / C + (x1 is not None and s1 is None) * c1 / C
+    _prof_stop(ev, "group_norm", 0.0, passes * out.numel() * out.element_size(),
+               f"hw={hw} C={c0}+{c1} fused_stats={s0 is not None}")
     return out
 
 
