@@ -1,0 +1,116 @@
+#!/usr/bin/env python3
+"""Micro-benchmark single HIP ops at UNet shapes (for A/B of kernel variants and rocprofv3).
+
+    python tools/opbench.py [--iters N] [--only NAME ...]
+
+Prints one line per case: mean launch time (HIP events, current stream) and achieved
+TFLOP/s or GB/s.  All variants run interleaved in ONE process (MI355X_MICROARCH §5.4 rule 24).
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "video-latent-diffusion-panoptic-segmentation_amd"))
+
+import torch  # noqa: E402
+
+from ldmseg.ops import native as K  # noqa: E402
+
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, geglu=False, residual=False,
+              temb=False, stats=False, c1=0):
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x0 = torch.randn(B, H, W, Cin - c1, device=DEV, generator=g).to(BF)
+    x1 = torch.randn(B, H, W, c1, device=DEV, generator=g).to(BF) if c1 else None
+    w = torch.randn(Cout, Cin, k, k, device=DEV, generator=g) * 0.05
+    pc = K.PackedConv(w, torch.randn(Cout, device=DEV), BF, geglu=geglu)
+    ho, wo = (2 * H, 2 * W) if up else ((H - 1) // stride + 1, (W - 1) // stride + 1)
+    res = torch.randn(B, ho, wo, Cout, device=DEV).to(BF) if residual else None
+    te = torch.randn(B, Cout, device=DEV) if temb else None
+    out_layout = K.OUT_GEGLU if geglu else layout
+
+    def run():
+        return K.conv2d(pc, x0, B, H, W, x1=x1, stride=stride, upsample=up, residual=res, temb=te,
+                        temb_stride=Cout if temb else 0, out_layout=out_layout, gn_stats=stats)
+    flops = 2.0 * B * ho * wo * Cout * k * k * Cin
+    return run, flops, None
+
+
+def attn_case(B, N, C, heads=8):
+    qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
+
+    def run():
+        return K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, C // heads, N, N, 3 * C, 3 * C, 3 * C)
+    return run, 4.0 * B * heads * N * N * (C // heads), None
+
+
+def gn_case(B, HW, C, stats):
+    x = torch.randn(B, HW, C, device=DEV).to(BF)
+    if stats:
+        setattr(x, K.GN_PART_ATTR, torch.zeros(B * HW // 64, C, 2, device=DEV))
+    gam, bet = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+
+    def run():
+        return K.group_norm(x, B, HW, 32, gam, bet, 1e-5, K.ACT_SILU)
+    return run, None, (2 + (0 if stats else 1)) * x.numel() * 2
+
+
+def ln_case(rows, C):
+    x = torch.randn(rows, C, device=DEV).to(BF)
+    gam, bet = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    return (lambda: K.layer_norm(x, gam, bet, 1e-5)), None, 2 * x.numel() * 2
+
+
+CASES = {
+    "conv3_l0_320": lambda: conv_case(8, 64, 64, 320, 320, temb=True, stats=True),
+    "conv3_l1_640": lambda: conv_case(8, 32, 32, 640, 640, temb=True, stats=True),
+    "conv3_l2_1280": lambda: conv_case(8, 16, 16, 1280, 1280, temb=True, stats=True),
+    "conv3_l3_1280": lambda: conv_case(8, 8, 8, 1280, 1280, temb=True, stats=True),
+    "conv3_up_l0_960": lambda: conv_case(8, 64, 64, 960, 320, c1=320, residual=True, stats=True),
+    "conv3_upsample_640": lambda: conv_case(8, 32, 32, 640, 640, up=True, stats=True),
+    "gemm_proj_320": lambda: conv_case(8, 64, 64, 320, 320, k=1, residual=True),
+    "gemm_qkv_320": lambda: conv_case(8, 64, 64, 320, 960, k=1),
+    "gemm_geglu_320": lambda: conv_case(8, 64, 64, 320, 2560, k=1, geglu=True),
+    "gemm_ff2_1280": lambda: conv_case(8, 64, 64, 1280, 320, k=1, residual=True),
+    "gemm_geglu_1280": lambda: conv_case(8, 16, 16, 1280, 10240, k=1, geglu=True),
+    "attn_4096_d40": lambda: attn_case(8, 4096, 320),
+    "attn_1024_d80": lambda: attn_case(8, 1024, 640),
+    "attn_256_d160": lambda: attn_case(8, 256, 1280),
+    "gn_l0_fused": lambda: gn_case(8, 4096, 320, True),
+    "gn_l0_unfused": lambda: gn_case(8, 4096, 320, False),
+    "ln_l0": lambda: ln_case(32768, 320),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only", nargs="*")
+    a = ap.parse_args()
+    names = a.only or list(CASES)
+    built = {n: CASES[n]() for n in names}
+    for n, (run, _, _) in built.items():
+        run()
+    torch.cuda.synchronize()
+    res = {n: [] for n in names}
+    for rnd in range(3):
+        for n, (run, _, _) in built.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            res[n].append(e0.elapsed_time(e1) / a.iters)
+    for n, (run, flops, nbytes) in built.items():
+        ms = min(res[n])
+        perf = f"{flops / ms / 1e9:8.1f} TF/s" if flops else f"{nbytes / ms / 1e6:8.1f} GB/s"
+        print(f"{n:22s} {ms * 1e3:9.1f} us  {perf}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -35,8 +35,21 @@ template <> __device__ __forceinline__ float from_f<float>(float v) { return v; 
 template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return f2bf(v); }
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
-__device__ __forceinline__ float gelu_f(float x) {  // exact (erf) GELU, torch approximate='none'
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+// erf via Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 absolute): one v_rcp, one v_exp and a
+// degree-5 Horner chain instead of ocml erff's ~40-instruction path.
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
+  float y = fmaf(1.061405429f, t, -1.453152027f);
+  y = fmaf(y, t, 1.421413741f);
+  y = fmaf(y, t, -0.284496736f);
+  y = fmaf(y, t, 0.254829592f);
+  y *= t;
+  const float e = __builtin_amdgcn_exp2f(-ax * ax * 1.4426950408889634f);
+  return copysignf(fmaf(-y, e, 1.0f), x);
+}
+__device__ __forceinline__ float gelu_f(float x) {  // exact-form (erf) GELU, torch approximate='none'
+  return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

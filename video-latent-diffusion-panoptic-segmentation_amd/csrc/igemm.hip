@@ -104,10 +104,8 @@ __device__ __forceinline__ void load4(const char* base, int64_t idx, float* v) {
 // Finish 4 consecutive output channels [n, n+4) of row m from raw accumulators:
 // bias, time embedding, activation, residual, store.  `v` returns the stored values.
 template <typename T>
-__device__ __forceinline__ void finish4(const ConvArgs& p, int m, int n, float* v) {
+__device__ __forceinline__ void finish4(const ConvArgs& p, int m, int b, int pix, int n, float* v) {
   const int N = p.n;
-  const int b = m / p.hw_out;
-  const int pix = m - b * p.hw_out;
   const bool f32o = p.out_f32 != 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -171,26 +169,24 @@ __device__ __forceinline__ void finish_geglu4(const ConvArgs& p, int m, int oc, 
 
 // Phase 2 of the epilogue, shared by the fused path (raw values staged in LDS) and the
 // split-K reduction (raw values summed from the fp32 slab).  `raw(r, c4, v)` fills 4 raw
-// values of local row r, local 4-channel chunk c4.  Rows [0, ROWS), channels [0, COLS).
-// Threads sweep (row, chunk) with chunk fastest -> coalesced row segments.
-template <typename T, int ROWS, int COLS, typename RawFn>
+// values of local row r, local 4-channel chunk c4.  Rows [0, ROWS), channels [0, COLS),
+// NT threads.  Threads sweep (row, chunk) with chunk fastest -> coalesced row segments.
+// With gn_part set, per-channel (sum, sumsq) over each 64-row chunk of the stored values
+// is reduced through `red` ([RP][CW][ROWS/64][4][2] floats) and written to gn_part.
+template <typename T, int ROWS, int COLS, int NT, typename RawFn>
 __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0, RawFn raw, float* red) {
   constexpr int CW = COLS / 4;           // chunks per row
-  constexpr int RP = 256 / CW;           // rows per pass
+  constexpr int RP = NT / CW;            // rows per pass
   constexpr int HALVES = ROWS / 64 > 0 ? ROWS / 64 : 1;
   const int tid = threadIdx.x;
   const int c4 = tid % CW, r0 = tid / CW;
   const bool geglu = p.out_layout == LDM_OUT_GEGLU;
   const bool stats = p.gn_part != nullptr;
-  float s[HALVES][4], q[HALVES][4];
-#pragma unroll
-  for (int hh = 0; hh < HALVES; ++hh)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { s[hh][r] = 0.f; q[hh][r] = 0.f; }
   if (geglu) {
     constexpr int OCW = CW / 2;          // GEGLU output chunks per row (half width)
-    constexpr int ORP = 256 / OCW;
+    constexpr int ORP = NT / OCW;
     const int oc4 = tid % OCW, or0 = tid / OCW;
+    if (or0 >= ORP) return;
 #pragma unroll 2
     for (int r = or0; r < ROWS; r += ORP) {
       const int m = m0 + r;
@@ -205,37 +201,51 @@ __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0,
     }
     return;
   }
-#pragma unroll 2
-  for (int r = r0; r < ROWS; r += RP) {
-    const int m = m0 + r;
-    const int n = n0 + 4 * c4;
-    if (m >= p.M || n >= p.n) continue;
-    float v[4];
-    raw(r, c4, v);
-    finish4<T>(p, m, n, v);
-    if (stats) {
-      const int hh = HALVES > 1 ? (r >> 6) : 0;
+  float s[HALVES][4], q[HALVES][4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        // statistics of the value as stored (bf16-rounded on the bf16 path)
-        const float x = (sizeof(T) == 2 && !p.out_f32) ? bf2f(f2bf(v[k])) : v[k];
-        s[hh][k] += x;
-        q[hh][k] += x * x;
+  for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { s[hh][r] = 0.f; q[hh][r] = 0.f; }
+  if (r0 < RP) {
+    // (batch, pixel) of this thread's first row, then advanced by RP rows without divisions
+    int bb = (m0 + r0) / p.hw_out;
+    int pix = (m0 + r0) - bb * p.hw_out;
+#pragma unroll 2
+    for (int r = r0; r < ROWS; r += RP) {
+      const int m = m0 + r;
+      const int n = n0 + 4 * c4;
+      const int b_row = bb, pix_row = pix;
+      pix += RP;
+      while (pix >= p.hw_out) { pix -= p.hw_out; ++bb; }
+      if (m >= p.M || n >= p.n) continue;
+      float v[4];
+      raw(r, c4, v);
+      finish4<T>(p, m, b_row, pix_row, n, v);
+      if (stats) {
+        const int hh = HALVES > 1 ? (r >> 6) : 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // statistics of the value as stored (bf16-rounded on the bf16 path)
+          const float x = (sizeof(T) == 2 && !p.out_f32) ? bf2f(f2bf(v[k])) : v[k];
+          s[hh][k] += x;
+          q[hh][k] += x * x;
+        }
       }
     }
   }
   if (!stats) return;
-  // reduce over the RP row-groups that share a chunk column: red[RP][CW][HALVES][4][2]
   __syncthreads();
+  if (r0 < RP) {
 #pragma unroll
-  for (int hh = 0; hh < HALVES; ++hh)
+    for (int hh = 0; hh < HALVES; ++hh)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 0] = s[hh][k];
-      red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 1] = q[hh][k];
-    }
+      for (int k = 0; k < 4; ++k) {
+        red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 0] = s[hh][k];
+        red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 1] = q[hh][k];
+      }
+  }
   __syncthreads();
-  for (int e = tid; e < CW * HALVES * 4; e += 256) {
+  for (int e = tid; e < CW * HALVES * 4; e += NT) {
     const int k = e & 3, hh = (e >> 2) % HALVES, c = e / (4 * HALVES);
     const int n = n0 + 4 * c + k;
     const int chunk = (m0 >> 6) + hh;
@@ -516,7 +526,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     const float4 x = *reinterpret_cast<const float4*>(stage + r * PITCH + 4 * c4);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
   };
-  epilogue_rows<T, BM, BN>(p, m0, n0, raw, red);
+  epilogue_rows<T, BM, BN, 256>(p, m0, n0, raw, red);
 }
 
 // Split-K reduction + full epilogue: one block per 64-row x 128-channel tile.
@@ -541,7 +551,7 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) 
         for (int r2 = 0; r2 < 4 && n + r2 < p.n; ++r2) v[r2] += src[s * slab + r2];
     }
   };
-  epilogue_rows<T, 64, 128>(p, m0, n0, raw, red);
+  epilogue_rows<T, 64, 128, 256>(p, m0, n0, raw, red);
 }
 
 template <typename T, int BM, int BN>
