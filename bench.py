@@ -87,11 +87,30 @@ def roofline(unet, stepper, ts, nsteps, dtype):
         achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9
         rl = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
               "frac": round(achieved / PEAK_HBM_GBS, 4)}
-    rl["traffic"] = None
+    rl["traffic"], rl["traffic_source"] = pmc_traffic(dom)
     rl["avg_launch_ms"] = round(d["ms"] / d["launches"], 5)
-    rl["algorithmic_per_launch"] = round((d["flops"] or d["bytes"]) / d["launches"], 1)
+    rl["launches_per_step"] = d["launches"] // nsteps
+    rl["algorithmic_flops_per_launch"] = round(d["flops"] / d["launches"], 1)
+    rl["algorithmic_bytes_per_launch"] = round(d["bytes"] / d["launches"], 1)
     rl["kernels_per_step"] = per_step
     return rl
+
+
+def pmc_traffic(family):
+    """HBM bytes per launch of `family` from the newest committed PMC summary
+    (profiles/rNN_families.json, written by tools/profile_bench.sh from separate FETCH_SIZE /
+    WRITE_SIZE rocprofv3 passes over this same command).  A live bench run cannot read PMC
+    counters itself; None when no summary exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_families.json")))
+    for f in reversed(files):
+        try:
+            fam = json.load(open(f))["families"].get(family, {})
+        except (OSError, ValueError, KeyError):
+            continue
+        if "traffic_bytes_per_call" in fam:
+            return fam["traffic_bytes_per_call"], os.path.relpath(f, ROOT)
+    return None, None
 
 
 def cpu_baseline(unet, budget_s=25.0):

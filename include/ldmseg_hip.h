@@ -85,6 +85,11 @@ typedef struct {
 /* Deep-K / few-tile shapes are split over K into an fp32 slab; this returns its size (0: none). */
 size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* p);
 int ldm_conv2d(const ldm_conv_params* p, ldm_stream_t stream);
+/* Tuning hook (benchmarks and tests only, not thread-safe): force the tile plan of every
+ * following ldm_conv2d call where it is legal — bm in {32, 64, 128} x bn in {32, 64, 128},
+ * or bm = 256 for the large-tile bf16 kernel (bn 160); ksplit >= 1 (clamped).  bm = 0
+ * restores the built-in heuristic.  Query ldm_conv2d_workspace_bytes after forcing. */
+void ldm_conv2d_force_plan(int bm, int bn, int ksplit);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).

@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _declared_symbols():
     src = open(os.path.join(ROOT, "include", "ldmseg_hip.h")).read()
-    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(ldm_\w+)\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:int|void|size_t|const char\*)\s+(ldm_\w+)\(", src, re.M)))
 
 
 def test_library_loads_and_exports_every_declared_symbol():
@@ -159,3 +159,12 @@ def test_vae_state_dict_keys_match_reference(cname):
     v = GeneralVAESeg(**VAE_CONFIGS[cname])
     assert list(v.state_dict().keys()) == list(z[f"{cname}__keys"])
     assert v.interpolation_factor == int(z[f"{cname}__interpolation_factor"])
+
+
+def test_alias_package_imports_next_to_reference_name():
+    """the drop-in modules load as ``ldmseg_mi355x`` (no GPU needed)."""
+    import importlib
+    m = importlib.import_module("ldmseg_mi355x")
+    from ldmseg_mi355x.models import GeneralVAESeg, UNet  # noqa: F401
+    from ldmseg_mi355x.schedulers import DDIMNoiseScheduler  # noqa: F401
+    assert m.__name__ == "ldmseg_mi355x" and UNet.__module__ == "ldmseg_mi355x.models.unet"

@@ -1,0 +1,128 @@
+"""ldm_conv2d under every tile plan (forced through ldm_conv2d_force_plan) vs torch fp32.
+
+The built-in planner picks one plan per shape; these tests run the SAME shapes through each
+kernel variant — the 256x160 three-stage bf16 kernel (with and without split-K) and the
+128/64/32 tile kernels — so a variant the planner does not pick for the test sizes is still
+covered.  Tolerance: bf16 storage, fp32 accumulate -> 2e-2 of the tensor scale (the same bar
+as tests/test_gpu_ops.py); fp32 -> 1e-4.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from ldmseg.ops import native as K
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+BF = torch.bfloat16
+
+
+def rel_err(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+@pytest.fixture
+def plan():
+    def set_plan(bm, bn, ks):
+        K.force_conv_plan(bm, bn, ks)
+    yield set_plan
+    K.force_conv_plan(0, 0, 1)
+
+
+PLANS = [(256, 160, 1), (256, 160, 3), (128, 128, 1), (128, 32, 2), (64, 64, 1), (32, 128, 3)]
+SHAPES = [
+    # name, B, c0, c1, H, W, Cout, k, stride, upsample
+    ("l0", 1, 320, 0, 32, 32, 320, 3, 1, False),
+    ("ragged_m_n", 1, 64, 0, 20, 20, 200, 3, 1, False),
+    ("concat", 2, 128, 64, 9, 9, 160, 3, 1, False),
+    ("upsample", 1, 128, 0, 8, 6, 192, 3, 1, True),
+    ("stride2", 2, 64, 0, 17, 15, 96, 3, 2, False),
+    ("pointwise", 3, 320, 0, 10, 10, 960, 1, 1, False),
+    ("deep_k", 2, 1280, 0, 8, 8, 320, 3, 1, False),
+]
+
+
+@pytest.mark.parametrize("pl", PLANS, ids=[f"{a}x{b}_k{c}" for a, b, c in PLANS])
+@pytest.mark.parametrize("case", SHAPES, ids=[s[0] for s in SHAPES])
+def test_conv_plan(case, pl, plan):
+    name, B, c0, c1, H, W, Co, k, s, up = case
+    torch.manual_seed(3)
+    x = torch.randn(B, c0 + c1, H, W)
+    w = torch.randn(Co, c0 + c1, k, k) / (k * (c0 + c1) ** 0.5)
+    b = torch.randn(Co)
+    temb = torch.randn(B, Co)
+    xr = F.interpolate(x, scale_factor=2.0, mode="nearest") if up else x
+    ref = F.silu(F.conv2d(xr, w, b, stride=s, padding=k // 2) + temb[:, :, None, None])
+    resid = torch.randn_like(ref)
+    ref = ref + resid
+    pc = K.PackedConv(w.to(DEV), b.to(DEV), BF)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV, BF)
+    x0 = xn[..., :c0].contiguous()
+    x1 = xn[..., c0:].contiguous() if c1 else None
+    plan(*pl)
+    out = K.conv2d(pc, x0, B, H, W, x1=x1, stride=s, upsample=up, temb=temb.to(DEV), temb_stride=Co,
+                   residual=resid.permute(0, 2, 3, 1).contiguous().to(DEV, BF), act=K.ACT_SILU)
+    assert rel_err(out.permute(0, 3, 1, 2), ref) < 2e-2
+
+
+@pytest.mark.parametrize("pl", PLANS, ids=[f"{a}x{b}_k{c}" for a, b, c in PLANS])
+def test_plan_groupnorm_stats(pl, plan):
+    """Epilogue GroupNorm partials (two 128-row halves in the large kernel, split-K reduce)."""
+    B, H, C, Co, G = 2, 16, 192, 320, 32
+    torch.manual_seed(4)
+    x = torch.randn(B, C, H, H)
+    w = torch.randn(Co, C, 3, 3) / (3 * C ** 0.5)
+    b = torch.randn(Co)
+    y_ref = F.conv2d(x, w, b, padding=1)
+    pc = K.PackedConv(w.to(DEV), b.to(DEV), BF)
+    plan(*pl)
+    y = K.conv2d(pc, x.permute(0, 2, 3, 1).contiguous().to(DEV, BF), B, H, H, gn_stats=True)
+    assert K.gn_stats_of(y) is not None
+    gam, bet = torch.randn(Co), torch.randn(Co)
+    out = K.group_norm(y, B, H * H, G, gam.to(DEV), bet.to(DEV), 1e-5, K.ACT_SILU)
+    ref = F.silu(F.group_norm(y_ref, G, gam, bet, 1e-5))
+    assert rel_err(out.view(B, H, H, -1).permute(0, 3, 1, 2), ref) < 3e-2
+
+
+@pytest.mark.parametrize("pl", [(256, 160, 1), (128, 128, 1), (64, 64, 1)], ids=["256x160", "128x128", "64x64"])
+@pytest.mark.parametrize("M,Kd,N", [(300, 320, 2560), (1024, 640, 640)])
+def test_plan_geglu(M, Kd, N, pl, plan):
+    torch.manual_seed(5)
+    x = torch.randn(M, Kd)
+    lin = torch.nn.Linear(Kd, N)
+    with torch.no_grad():
+        h, gate = lin(x).chunk(2, dim=-1)
+    pg = K.PackedConv(lin.weight.to(DEV), lin.bias.to(DEV), BF, geglu=True)
+    plan(*pl)
+    g = K.linear(pg, x.to(DEV, BF), out_layout=K.OUT_GEGLU)
+    assert rel_err(g, h * F.gelu(gate)) < 2e-2
+
+
+@pytest.mark.parametrize("pl", [(256, 160, 1), (128, 128, 1)], ids=["256x160", "128x128"])
+def test_plan_shuffle2(pl, plan):
+    """ConvTranspose2d(k2, s2) as GEMM + pixel-shuffle epilogue (seg-VAE decoder)."""
+    torch.manual_seed(6)
+    B, C, H, W, Co = 2, 256, 12, 20, 80
+    x = torch.randn(B, C, H, W)
+    ct = torch.nn.ConvTranspose2d(C, Co, 2, stride=2)
+    with torch.no_grad():
+        ref = ct(x)
+    pc = K.PackedConv(ct.weight.to(DEV), ct.bias.to(DEV), BF, shuffle2=True)
+    plan(*pl)
+    y = K.conv2d(pc, x.permute(0, 2, 3, 1).contiguous().to(DEV, BF), B, H, W, out_layout=K.OUT_SHUFFLE2)
+    assert rel_err(y.permute(0, 3, 1, 2), ref) < 2e-2
+
+
+def test_planner_picks_large_tiles_for_level0(plan):
+    """With no override the level-0 UNet conv goes to the large-tile kernel (observable as a
+    zero split-K workspace and identical output to the forced large-tile plan)."""
+    torch.manual_seed(7)
+    B, C, H = 8, 320, 64
+    x = torch.randn(B, H, H, C, device=DEV).to(BF)
+    w = torch.randn(C, C, 3, 3, device=DEV) * 0.02
+    pc = K.PackedConv(w, torch.zeros(C, device=DEV), BF)
+    y_auto = K.conv2d(pc, x, B, H, H)
+    plan(256, 160, 1)
+    y_big = K.conv2d(pc, x, B, H, H)
+    assert torch.equal(y_auto, y_big)

@@ -77,6 +77,13 @@ CASES = {
     "gemm_geglu_320": lambda: conv_case(8, 64, 64, 320, 2560, k=1, geglu=True),
     "gemm_ff2_1280": lambda: conv_case(8, 64, 64, 1280, 320, k=1, residual=True),
     "gemm_geglu_1280": lambda: conv_case(8, 16, 16, 1280, 10240, k=1, geglu=True),
+    "gemm_qkv_640": lambda: conv_case(8, 32, 32, 640, 1920, k=1),
+    "gemm_geglu_640": lambda: conv_case(8, 32, 32, 640, 5120, k=1, geglu=True),
+    "gemm_ff2_2560": lambda: conv_case(8, 32, 32, 2560, 640, k=1, residual=True),
+    "gemm_proj_640": lambda: conv_case(8, 32, 32, 640, 640, k=1, residual=True),
+    "conv3_up_l1_1920": lambda: conv_case(8, 32, 32, 1920, 640, c1=640, residual=True, stats=True),
+    "conv3_upsample_320": lambda: conv_case(8, 32, 32, 640, 640, up=True, stats=True),
+    "conv3_l2_up_2560": lambda: conv_case(8, 16, 16, 2560, 1280, c1=1280, residual=True, stats=True),
     "attn_4096_d40": lambda: attn_case(8, 4096, 320),
     "attn_1024_d80": lambda: attn_case(8, 1024, 640),
     "attn_256_d160": lambda: attn_case(8, 256, 1280),
@@ -90,13 +97,27 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", nargs="*")
+    ap.add_argument("--plans", nargs="*", default=["auto"],
+                    help="conv tile plans to compare: 'auto' or 'bm,bn,ksplit' (e.g. 256,160,1)")
     a = ap.parse_args()
     names = a.only or list(CASES)
-    built = {n: CASES[n]() for n in names}
+    built = {}
+    for n in names:
+        if not n.startswith(("conv", "gemm")):
+            built[n] = CASES[n]()
+            continue
+        for pl in a.plans:
+            run, fl, nb = CASES[n]()
+            bm, bn, ks = (0, 0, 1) if pl == "auto" else map(int, pl.split(","))
+
+            def run_pl(run=run, bm=bm, bn=bn, ks=ks):
+                K.force_conv_plan(bm, bn, ks)
+                return run()
+            built[n if pl == "auto" else f"{n}@{pl}"] = (run_pl, fl, nb)
     for n, (run, _, _) in built.items():
         run()
     torch.cuda.synchronize()
-    res = {n: [] for n in names}
+    res = {n: [] for n in built}
     for rnd in range(3):
         for n, (run, _, _) in built.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

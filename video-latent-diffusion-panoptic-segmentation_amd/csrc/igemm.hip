@@ -101,18 +101,17 @@ __device__ __forceinline__ void load4(const char* base, int64_t idx, float* v) {
   }
 }
 
-// Finish 4 consecutive output channels [n, n+4) of row m from raw accumulators:
-// bias, time embedding, activation, residual, store.  `v` returns the stored values.
+// Finish 4 consecutive output channels [n, n+4) of row m from raw accumulators: + bias,
+// + time embedding (both preloaded by the caller: they depend only on the column / batch),
+// activation, + residual (NHWC: preloaded into `res`), store.  `v` returns the stored values.
 template <typename T>
-__device__ __forceinline__ void finish4(const ConvArgs& p, int m, int b, int pix, int n, float* v) {
+__device__ __forceinline__ void finish4(const ConvArgs& p, int b, int pix, int m, int n, float* v,
+                                        const float* bias4, const float* temb4, const float* res) {
   const int N = p.n;
   const bool f32o = p.out_f32 != 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int nn = min(n + r, N - 1);
-    float x = v[r];
-    if (p.bias) x += p.bias[nn];
-    if (p.temb) x += p.temb[(int64_t)b * p.temb_stride + nn];
+    float x = v[r] + bias4[r] + temb4[r];
     if (p.act == LDM_ACT_SILU) x = silu_f(x);
     v[r] = x;
   }
@@ -129,106 +128,148 @@ __device__ __forceinline__ void finish4(const ConvArgs& p, int m, int b, int pix
   int64_t idx;
   if (p.out_layout == LDM_OUT_NHWC) {
     idx = (int64_t)m * N + n;
+    if (p.residual) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] += res[r];
+    }
   } else {  // LDM_OUT_SHUFFLE2: n = (dy*2+dx)*Cout + co -> output pixel (2y+dy, 2x+dx)
     const int cout = N >> 2;
     const int qd = n / cout, co = n - qd * cout;
     const int y = pix / p.w_out, x = pix - y * p.w_out;
     idx = (((int64_t)b * 2 * p.h_out + 2 * y + (qd >> 1)) * 2 * p.w_out + 2 * x + (qd & 1)) * cout + co;
+    if (p.residual) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < N) v[r] += to_f(reinterpret_cast<const T*>(p.residual)[idx + r]);
+    }
   }
   if (n + 3 < N) {
-    if (p.residual) {
-      float rv[4];
-      load4<T>(p.residual, idx, rv);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += rv[r];
-    }
     store4<T>(p.out, idx, v, f32o);
   } else {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (n + r >= N) { v[r] = 0.f; continue; }
-      if (p.residual) v[r] += to_f(reinterpret_cast<const T*>(p.residual)[idx + r]);
       store1<T>(p.out, idx + r, v[r], f32o);
     }
   }
 }
 
-// GEGLU: out[m, oc..oc+3] = (h + bh) * gelu(g + bg); packed columns: 16 hidden then 16 gate
-template <typename T>
-__device__ __forceinline__ void finish_geglu4(const ConvArgs& p, int m, int oc, const float* h, const float* gt) {
-  const int pc = (oc >> 4) * 32 + (oc & 15);
-  float v[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const float hh = h[r] + (p.bias ? p.bias[pc + r] : 0.f);
-    const float gg = gt[r] + (p.bias ? p.bias[pc + 16 + r] : 0.f);
-    v[r] = hh * gelu_f(gg);
-  }
-  store4<T>(p.out, (int64_t)m * (p.n >> 1) + oc, v, p.out_f32 != 0);
-}
-
 // Phase 2 of the epilogue, shared by the fused path (raw values staged in LDS) and the
 // split-K reduction (raw values summed from the fp32 slab).  `raw(r, c4, v)` fills 4 raw
 // values of local row r, local 4-channel chunk c4.  Rows [0, ROWS), channels [0, COLS),
-// NT threads.  Threads sweep (row, chunk) with chunk fastest -> coalesced row segments.
+// NT threads.  Threads sweep (row, chunk) with chunk fastest -> coalesced row segments; a
+// thread's columns are fixed, so bias (and the time embedding per batch) are loaded once,
+// and rows go in groups of GP whose raw values and residuals are all fetched before any is
+// finished — the global loads of a group overlap instead of forming a latency chain.
 // With gn_part set, per-channel (sum, sumsq) over each 64-row chunk of the stored values
 // is reduced through `red` ([RP][CW][ROWS/64][4][2] floats) and written to gn_part.
 template <typename T, int ROWS, int COLS, int NT, typename RawFn>
 __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0, RawFn raw, float* red) {
   constexpr int CW = COLS / 4;           // chunks per row
   constexpr int RP = NT / CW;            // rows per pass
+  constexpr int NP = (ROWS + RP - 1) / RP;
+  constexpr int GP = 4;                  // rows in flight per thread
   constexpr int HALVES = ROWS / 64 > 0 ? ROWS / 64 : 1;
   const int tid = threadIdx.x;
   const int c4 = tid % CW, r0 = tid / CW;
-  const bool geglu = p.out_layout == LDM_OUT_GEGLU;
+  const int N = p.n;
   const bool stats = p.gn_part != nullptr;
-  if (geglu) {
+  if (p.out_layout == LDM_OUT_GEGLU) {
     constexpr int OCW = CW / 2;          // GEGLU output chunks per row (half width)
     constexpr int ORP = NT / OCW;
+    constexpr int ONP = (ROWS + ORP - 1) / ORP;
     const int oc4 = tid % OCW, or0 = tid / OCW;
-    if (or0 >= ORP) return;
-#pragma unroll 2
-    for (int r = or0; r < ROWS; r += ORP) {
-      const int m = m0 + r;
-      const int oc = (n0 >> 1) + 4 * oc4;
-      if (m >= p.M || oc >= (p.n >> 1)) continue;
-      const int lc = 4 * oc4;                       // local output column
-      const int pcl = (lc >> 4) * 32 + (lc & 15);   // local packed column of the hidden half
-      float h[4], gt[4];
-      raw(r, pcl >> 2, h);
-      raw(r, (pcl + 16) >> 2, gt);
-      finish_geglu4<T>(p, m, oc, h, gt);
+    const int oc = (n0 >> 1) + 4 * oc4;
+    if (or0 >= ORP || oc >= (N >> 1)) return;
+    const int lc = 4 * oc4;                       // local output column
+    const int pcl = (lc >> 4) * 32 + (lc & 15);   // local packed column of the hidden half
+    const int pc = (oc >> 4) * 32 + (oc & 15);    // global packed column
+    float bh[4], bg[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      bh[k] = p.bias ? p.bias[pc + k] : 0.f;
+      bg[k] = p.bias ? p.bias[pc + 16 + k] : 0.f;
+    }
+#pragma unroll
+    for (int q0 = 0; q0 < ONP; q0 += GP) {
+      float h[GP][4], gt[GP][4];
+#pragma unroll
+      for (int q = 0; q < GP; ++q) {
+        const int r = or0 + (q0 + q) * ORP;
+        if (q0 + q < ONP && r < ROWS) {
+          raw(r, pcl >> 2, h[q]);
+          raw(r, (pcl + 16) >> 2, gt[q]);
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < GP; ++q) {
+        const int r = or0 + (q0 + q) * ORP;
+        if (q0 + q >= ONP || r >= ROWS || m0 + r >= p.M) continue;
+        float v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = (h[q][k] + bh[k]) * gelu_f(gt[q][k] + bg[k]);
+        store4<T>(p.out, (int64_t)(m0 + r) * (N >> 1) + oc, v, p.out_f32 != 0);
+      }
     }
     return;
   }
-  float s[HALVES][4], q[HALVES][4];
+  float s[HALVES][4], sq[HALVES][4];
 #pragma unroll
   for (int hh = 0; hh < HALVES; ++hh)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) { s[hh][r] = 0.f; q[hh][r] = 0.f; }
-  if (r0 < RP) {
+    for (int k = 0; k < 4; ++k) { s[hh][k] = 0.f; sq[hh][k] = 0.f; }
+  const int n = n0 + 4 * c4;
+  if (r0 < RP && n < N) {
+    float bias4[4], temb4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) bias4[k] = p.bias ? p.bias[min(n + k, N - 1)] : 0.f;
+    int tb = -1;                                   // batch whose temb4 is loaded
+    const bool nhwc_res = p.residual && p.out_layout == LDM_OUT_NHWC;
     // (batch, pixel) of this thread's first row, then advanced by RP rows without divisions
     int bb = (m0 + r0) / p.hw_out;
     int pix = (m0 + r0) - bb * p.hw_out;
-#pragma unroll 2
-    for (int r = r0; r < ROWS; r += RP) {
-      const int m = m0 + r;
-      const int n = n0 + 4 * c4;
-      const int b_row = bb, pix_row = pix;
-      pix += RP;
-      while (pix >= p.hw_out) { pix -= p.hw_out; ++bb; }
-      if (m >= p.M || n >= p.n) continue;
-      float v[4];
-      raw(r, c4, v);
-      finish4<T>(p, m, b_row, pix_row, n, v);
-      if (stats) {
-        const int hh = HALVES > 1 ? (r >> 6) : 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          // statistics of the value as stored (bf16-rounded on the bf16 path)
-          const float x = (sizeof(T) == 2 && !p.out_f32) ? bf2f(f2bf(v[k])) : v[k];
-          s[hh][k] += x;
-          q[hh][k] += x * x;
+    for (int q0 = 0; q0 < NP; q0 += GP) {
+      float v[GP][4], rv[GP][4];
+      int bq[GP], pq[GP];
+#pragma unroll
+      for (int q = 0; q < GP; ++q) {
+        const int r = r0 + (q0 + q) * RP;
+        bq[q] = bb; pq[q] = pix;
+        pix += RP;
+        while (pix >= p.hw_out) { pix -= p.hw_out; ++bb; }
+        if (q0 + q >= NP || r >= ROWS || m0 + r >= p.M) continue;
+        raw(r, c4, v[q]);
+        if (nhwc_res) {
+          const int64_t idx = (int64_t)(m0 + r) * N + n;
+          if (n + 3 < N) {
+            load4<T>(p.residual, idx, rv[q]);
+          } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              rv[q][k] = n + k < N ? to_f(reinterpret_cast<const T*>(p.residual)[idx + k]) : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < GP; ++q) {
+        const int r = r0 + (q0 + q) * RP;
+        if (q0 + q >= NP || r >= ROWS || m0 + r >= p.M) continue;
+        if (p.temb && bq[q] != tb) {
+          tb = bq[q];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) temb4[k] = p.temb[(int64_t)tb * p.temb_stride + min(n + k, N - 1)];
+        }
+        finish4<T>(p, bq[q], pq[q], m0 + r, n, v[q], bias4, temb4, rv[q]);
+        if (stats) {
+          const int hh = HALVES > 1 ? (r >> 6) : 0;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            // statistics of the value as stored (bf16-rounded on the bf16 path)
+            const float x = (sizeof(T) == 2 && !p.out_f32) ? bf2f(f2bf(v[q][k])) : v[q][k];
+            s[hh][k] += x;
+            sq[hh][k] += x * x;
+          }
         }
       }
     }
@@ -241,21 +282,21 @@ __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0,
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 0] = s[hh][k];
-        red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 1] = q[hh][k];
+        red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 1] = sq[hh][k];
       }
   }
   __syncthreads();
   for (int e = tid; e < CW * HALVES * 4; e += NT) {
     const int k = e & 3, hh = (e >> 2) % HALVES, c = e / (4 * HALVES);
-    const int n = n0 + 4 * c + k;
+    const int nn = n0 + 4 * c + k;
     const int chunk = (m0 >> 6) + hh;
-    if (n >= p.n || chunk * 64 >= p.M) continue;
+    if (nn >= N || chunk * 64 >= p.M) continue;
     float a = 0.f, b = 0.f;
     for (int rg = 0; rg < RP; ++rg) {
       a += red[(((rg * CW + c) * HALVES + hh) * 4 + k) * 2 + 0];
       b += red[(((rg * CW + c) * HALVES + hh) * 4 + k) * 2 + 1];
     }
-    p.gn_part[(int64_t)chunk * p.n + n] = make_float2(a, b);
+    p.gn_part[(int64_t)chunk * N + nn] = make_float2(a, b);
   }
 }
 
@@ -554,6 +595,226 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) 
   epilogue_rows<T, 64, 128, 256>(p, m0, n0, raw, red);
 }
 
+// ---------------------------------------------------------------------------------------
+// Large-tile bf16 kernel for the big UNet GEMMs (64x64 / 32x32 levels, GEGLU, QKV).
+// Block tile 256 x 160 (160 divides every SD channel count: 320, 640, 960, 1280, 2560 ...),
+// 512 threads = 8 waves as 4 (M) x 2 (N), wave tile 64 x 80 = 4 x 5 fragments, so LDS reads
+// per MFMA drop ~10 % and LDS-DMA writes per MFMA ~35 % against the 128 x 128 kernel.
+// Operands stream through a 3-stage LDS-DMA ring (3 x 52 KiB): tile k+2 is in flight while
+// tile k is multiplied, and each wave waits only for its own oldest tile with a counted
+// vmcnt (7 or 6 LDS-DMA instructions per tile depending on the wave), then one barrier.
+// ---------------------------------------------------------------------------------------
+namespace big {
+constexpr int BM = 256, BN = 160, BK = 64, NT = 512;
+constexpr int STAGE_U4 = (BM + BN) * 8;          // uint4 per ring stage (53,248 B)
+constexpr int NSTAGE = 3;
+constexpr int EPI_ROWS = 128;                      // epilogue staged in two row halves
+constexpr int PITCH = BN + 4;
+constexpr int RED_FLOATS = (NT / (BN / 4)) * (BN / 4) * (EPI_ROWS / 64) * 4 * 2;
+static_assert(EPI_ROWS * PITCH + RED_FLOATS <= NSTAGE * STAGE_U4 * 4, "epilogue does not fit the ring");
+}  // namespace big
+
+template <int MODE>   // experiment: 0 normal, 1 no operand loads, 2 no MFMA
+__global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
+  using namespace big;
+  typedef bf16_t T;
+  constexpr int ES = 2, CE = 8;
+  constexpr int AI = BM / 64;    // A rows per lane per stage (rows rr + 64 i)
+  constexpr int FM = 4, FN = 5;
+  __shared__ uint4 smem[NSTAGE * STAGE_U4];
+
+  int tile;
+  {
+    const int bid = blockIdx.x, nblk = p.nblk;
+    const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
+    tile = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+  }
+  const int split = tile % p.ksplit;
+  tile /= p.ksplit;
+  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk_all = p.kpad / BK;
+  const int kt0 = (int)((int64_t)nk_all * split / p.ksplit);
+  const int kt1 = (int)((int64_t)nk_all * (split + 1) / p.ksplit);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int cc = tid & 7, rr = tid >> 3;           // rr in [0, 64)
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+
+  const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)p.a0, 0, p.a0_bytes, kBufFlags);
+  const __amdgpu_buffer_rsrc_t ra1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.a1 ? p.a1 : p.a0), 0, p.a1 ? p.a1_bytes : 0, kBufFlags);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, p.w_bytes, kBufFlags);
+
+  int pix0[AI], iy0[AI], ix0[AI];
+  bool rok[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int m = m0 + rr + 64 * i;
+    rok[i] = m < p.M;
+    const int b = m / p.hw_out;
+    const int pix = m - b * p.hw_out;
+    const int oy = pix / p.w_out, ox = pix - oy * p.w_out;
+    if (p.upsample) {
+      iy0[i] = oy - p.pad;
+      ix0[i] = ox - p.pad;
+      pix0[i] = b * p.h_in;
+    } else {
+      iy0[i] = oy * p.stride - p.pad;
+      ix0[i] = ox * p.stride - p.pad;
+      pix0[i] = (b * p.h_in + iy0[i]) * p.w_in + ix0[i];
+    }
+  }
+  // source-side swizzle: (row >> 1) & 7 is the same for every row this lane loads
+  const int cl = cc ^ ((rr >> 1) & 7);
+  int ch = kt0 * BK + cl * CE, tap = ch / p.cin;
+  ch -= tap * p.cin;
+  int ky = tap / p.ksize, kx = tap - ky * p.ksize;
+  const int ntaps = p.ksize * p.ksize;
+
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+  const bool b_extra = wv < 4;                     // waves 0-3 also load B rows 128..159
+
+  auto issue = [&](int kt, int st) {
+    const unsigned abase = lds0 + (unsigned)(st * STAGE_U4 * 16);
+    const unsigned bbase = abase + BM * 128;
+    const bool kval = tap < ntaps;
+    const int sel = __builtin_amdgcn_readfirstlane((p.c1 > 0 && ch >= p.c0) ? 1 : 0);
+    const int cs = sel ? p.c1 : p.c0;
+    const int choff = sel ? ch - p.c0 : ch;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      int pixel;
+      bool ok = rok[i] && kval;
+      if (p.upsample) {
+        const int uy = iy0[i] + ky, ux = ix0[i] + kx;
+        ok = ok && (unsigned)uy < (unsigned)(2 * p.h_in) && (unsigned)ux < (unsigned)(2 * p.w_in);
+        pixel = (pix0[i] + (uy >> 1)) * p.w_in + (ux >> 1);
+      } else {
+        const int iy = iy0[i] + ky, ix = ix0[i] + kx;
+        ok = ok && (unsigned)iy < (unsigned)p.h_in && (unsigned)ix < (unsigned)p.w_in;
+        pixel = pix0[i] + ky * p.w_in + kx;
+      }
+      const int off = ok ? (pixel * cs + choff) * ES : kOOB;
+      const unsigned dst = __builtin_amdgcn_readfirstlane(abase + (64 * i + 8 * wv) * 128);
+      if (sel) dma16(ra1, off, dst);
+      else dma16(ra0, off, dst);
+    }
+    const int kb = (kt * BK + cl * CE) * ES;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i == 2 && !b_extra) break;
+      const int n = n0 + rr + 64 * i;
+      const int off = n < p.n ? n * p.kpad * ES + kb : kOOB;
+      dma16(rw, off, __builtin_amdgcn_readfirstlane(bbase + (64 * i + 8 * wv) * 128));
+    }
+    ch += BK;
+    while (ch >= p.cin) {
+      ch -= p.cin;
+      ++tap;
+      if (++kx == p.ksize) { kx = 0; ++ky; }
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, g = lane >> 4;
+  auto compute = [&](int st) {
+    const uint4* As = smem + st * STAGE_U4;
+    const uint4* Bs = As + BM * 8;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      Frag8<T> af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * 64 + i * 16 + lr;
+        af[i].v = As[r * 8 + swz(r, ks * 4 + g)];
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * 80 + j * 16 + lr;
+        bfr[j].v = Bs[r * 8 + swz(r, ks * 4 + g)];
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) mma_k32(acc[i][j], bfr[j], af[i]);
+    }
+  };
+
+  // ---- 3-stage ring: prologue fills stages 0 and 1
+  if (MODE != 1 && kt0 < kt1) issue(kt0, 0);
+  if (MODE != 1 && kt0 + 1 < kt1) issue(kt0 + 1, 1);
+  int st = 0;
+  for (int kt = kt0; kt < kt1; ++kt) {
+    if (kt + 1 < kt1) {           // leave tile kt+1's instructions in flight
+      if (b_extra) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // every wave's tile kt has landed, and every wave is done reading stage (kt-1) % 3
+    asm volatile("s_barrier" ::: "memory");
+    if (MODE != 1 && kt + 2 < kt1) issue(kt + 2, st == 0 ? 2 : st - 1);
+    if (MODE != 2) compute(st);
+    st = st == 2 ? 0 : st + 1;
+  }
+
+  if (p.ksplit > 1) {
+    float* part = p.partial + (int64_t)split * p.M * p.n;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int m = m0 + wm * 64 + i * 16 + lr;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * 80 + j * 16 + 4 * g;
+        if (n >= p.n) continue;
+        float* dst = part + (int64_t)m * p.n + n;
+        if (n + 3 < p.n) {
+          *reinterpret_cast<float4*>(dst) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        } else {
+          for (int r = 0; r < 4 && n + r < p.n; ++r) dst[r] = acc[i][j][r];
+        }
+      }
+    }
+    return;
+  }
+
+  // ---- fused epilogue, two halves of 128 rows (waves wm = 2h, 2h+1 own half h)
+  float* stage = reinterpret_cast<float*>(smem);
+  float* red = stage + EPI_ROWS * PITCH;
+  auto raw = [&](int r, int c4, float* v) {
+    const float4 x = *reinterpret_cast<const float4*>(stage + r * PITCH + 4 * c4);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  };
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();   // ring reads done (h = 0) / previous half consumed (h = 1)
+    if ((wm >> 1) == h) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ml = (wm & 1) * 64 + i * 16 + lr;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int nl = wn * 80 + j * 16 + 4 * g;
+          *reinterpret_cast<float4*>(stage + ml * PITCH + nl) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+      }
+    }
+    __syncthreads();
+    if (m0 + h * EPI_ROWS < p.M) epilogue_rows<T, EPI_ROWS, BN, NT>(p, m0 + h * EPI_ROWS, n0, raw, red);
+  }
+}
+
 template <typename T, int BM, int BN>
 int launch_bm_bn(ConvArgs a, hipStream_t s) {
   a.tiles_n = (a.n + BN - 1) / BN;
@@ -586,24 +847,67 @@ int launch_t(const ConvArgs& a, hipStream_t s, int bm, int bn) {
   return launch_bm<T, 128>(a, s, bn);
 }
 
+int g_big_mode = 0;
+int launch_big(ConvArgs a, hipStream_t s) {
+  a.tiles_n = (a.n + big::BN - 1) / big::BN;
+  const int tiles_m = (a.M + big::BM - 1) / big::BM;
+  a.nblk = tiles_m * a.tiles_n * a.ksplit;
+  if (g_big_mode == 1) hipLaunchKernelGGL(igemm_big_kernel<1>, dim3(a.nblk), dim3(big::NT), 0, s, a);
+  else if (g_big_mode == 2) hipLaunchKernelGGL(igemm_big_kernel<2>, dim3(a.nblk), dim3(big::NT), 0, s, a);
+  else hipLaunchKernelGGL(igemm_big_kernel<0>, dim3(a.nblk), dim3(big::NT), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  if (a.ksplit > 1) {
+    const int blocks = ((a.M + 63) / 64) * ((a.n + 127) / 128);
+    hipLaunchKernelGGL((splitk_epilogue_kernel<bf16_t>), dim3(blocks), dim3(256), 0, s, a);
+    LDM_CHECK_LAUNCH();
+  }
+  return LDM_OK;
+}
+
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 struct Plan {
-  int bm, bn, ksplit;
+  int bm, bn, ksplit;   // bm == 256: the large-tile bf16 kernel (bn 160)
 };
 
-Plan make_plan(const ldm_conv_params* q, int M, int es) {
+// Tuning override (ldm_conv2d_force_plan): applied when it is legal for the call.
+int g_force_bm = 0, g_force_bn = 0, g_force_ks = 0;
+
+int clamp_ksplit(int ks, int nk) { return std::max(1, std::min(std::min(ks, nk), 16)); }
+
+Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
   Plan pl;
+  const int bk = 128 / es;
+  const int nk = q->kpad / bk;
+  const bool split_ok = q->out_layout != LDM_OUT_GEGLU && q->out_layout != LDM_OUT_SHUFFLE2;
+  const bool big_ok = es == 2 && !mixed_src && q->out_layout != LDM_OUT_NCHW;
+  if (g_force_bm) {
+    const bool want_big = g_force_bm == 256;
+    if (!want_big || big_ok) {
+      pl.bm = want_big ? 256 : g_force_bm;
+      pl.bn = want_big ? 160 : g_force_bn;
+      pl.ksplit = split_ok ? clamp_ksplit(g_force_ks, nk) : 1;
+      if (q->out_layout == LDM_OUT_GEGLU && pl.bn < 64) pl.bn = 64;
+      return pl;
+    }
+  }
+  // Large tiles when they alone fill the chip and waste little of N.
+  if (big_ok) {
+    const int tn = (q->n + 159) / 160;
+    const int tiles = ((M + 255) / 256) * tn;
+    if (tiles >= 240 && tn * 160 * 10 <= q->n * 11) {
+      pl.bm = 256; pl.bn = 160; pl.ksplit = 1;
+      return pl;
+    }
+  }
   pl.bm = M <= 32 ? 32 : (M <= 64 ? 64 : 128);
   pl.bn = q->n <= 32 ? 32 : (q->n <= 64 ? 64 : 128);
   if (q->out_layout == LDM_OUT_GEGLU && pl.bn < 64) pl.bn = 64;
   pl.ksplit = 1;
   // Split K when the tile grid cannot fill the chip (the 8x8 / 16x16 UNet levels): aim for
   // ~2 blocks per CU, keep >= 8 K tiles per split.  Not for GEGLU / pixel-shuffle outputs.
-  const int bk = 128 / es;
-  const int nk = q->kpad / bk;
   const int tiles = ((M + pl.bm - 1) / pl.bm) * ((q->n + pl.bn - 1) / pl.bn);
-  if (q->out_layout != LDM_OUT_GEGLU && q->out_layout != LDM_OUT_SHUFFLE2 && tiles < 256 && nk >= 16) {
+  if (split_ok && tiles < 256 && nk >= 16) {
     int ks = (512 + tiles - 1) / tiles;
     ks = std::min(ks, nk / 8);
     ks = std::min(ks, 16);
@@ -647,13 +951,28 @@ int validate(const ldm_conv_params* q, int* es_out) {
   return LDM_OK;
 }
 
+// the concat boundary is not K-tile aligned: per-lane source select (register path)
+bool is_mixed(const ldm_conv_params* q, int es) {
+  const int bk = 128 / es;
+  return q->c1 > 0 && (q->c0 % bk || q->c1 % bk);
+}
+
 }  // namespace
+
+extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
+  g_big_mode = bm > 256 ? bm - 256 : 0;
+  if (bm > 256) bm = 256;
+  const bool ok = (bm == 256) || ((bm == 32 || bm == 64 || bm == 128) && (bn == 32 || bn == 64 || bn == 128));
+  g_force_bm = ok ? bm : 0;
+  g_force_bn = ok ? bn : 0;
+  g_force_ks = ok ? std::max(1, ksplit) : 0;
+}
 
 extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   int es = 0;
   if (validate(q, &es) != LDM_OK) return 0;
   const int M = q->batch * q->h_out * q->w_out;
-  const Plan pl = make_plan(q, M, es);
+  const Plan pl = make_plan(q, M, es, is_mixed(q, es));
   return pl.ksplit > 1 ? (size_t)pl.ksplit * M * q->n * sizeof(float) : 0;
 }
 
@@ -664,7 +983,8 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   const int bk = 128 / es;
   const int cin = q->c0 + q->c1;
   const int M = q->batch * q->h_out * q->w_out;
-  const Plan pl = make_plan(q, M, es);
+  const bool mixed = is_mixed(q, es);
+  const Plan pl = make_plan(q, M, es, mixed);
   if (pl.ksplit > 1) {
     const size_t need = (size_t)pl.ksplit * M * q->n * sizeof(float);
     if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;
@@ -689,10 +1009,11 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.M = M;
   a.tiles_n = 0;
   a.nblk = 0;
-  a.mixed_src = (q->c1 > 0 && (q->c0 % bk || q->c1 % bk)) ? 1 : 0;
+  a.mixed_src = mixed ? 1 : 0;
   a.ksplit = pl.ksplit;
   a.partial = static_cast<float*>(q->workspace);
   a.gn_part = reinterpret_cast<float2*>(q->gn_partial);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (pl.bm == 256) return launch_big(a, s);
   return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, s, pl.bm, pl.bn) : launch_t<float>(a, s, pl.bm, pl.bn);
 }

@@ -51,6 +51,7 @@ class DdimParams(ctypes.Structure):
 EXPORTS = {
     "ldm_conv2d": (_i, [ctypes.POINTER(ConvParams), _vp]),
     "ldm_conv2d_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(ConvParams)]),
+    "ldm_conv2d_force_plan": (None, [_i, _i, _i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_group_norm_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
     "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _i, _vp]),
@@ -304,6 +305,11 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
               f"Cin={c0}+{c1} L{out_layout}"
         _prof_stop(ev, "igemm", flops, nbytes, det)
     return out
+
+
+def force_conv_plan(bm=0, bn=0, ksplit=1):
+    """Tuning hook: force ldm_conv2d's tile plan (bm=256 -> large-tile bf16 kernel); bm=0 resets."""
+    load_library().ldm_conv2d_force_plan(int(bm), int(bn), int(ksplit))
 
 
 def linear(pc: PackedConv, x, **kw):
