@@ -183,11 +183,8 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        elapsed = te.item()
+    from ldmseg.utils import max_over_ranks
+    elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
     finite = bool(torch.isfinite(stepper.lat).all().item())
 
     rl = roofline(unet, stepper, ts, args.profile_steps, dtype) if rank == 0 else None

@@ -189,7 +189,9 @@ def test_group_norm(B, HW, c0, c1, G, eps, act, dt):
 
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("rows,C,eps,act", [(4096, 320, 1e-5, False), (333, 1280, 1e-5, False),
-                                            (1000, 256, 1e-6, True), (17, 2560, 1e-5, False)])
+                                            (1000, 256, 1e-6, True), (17, 2560, 1e-5, False),
+                                            (8191, 640, 1e-5, False), (5, 40, 1e-5, True),
+                                            (140001, 320, 1e-5, False)])   # > one grid-stride sweep
 def test_layer_norm(rows, C, eps, act, dt):
     torch.manual_seed(6)
     x = torch.randn(rows, C) * 2 - 0.5

@@ -84,12 +84,21 @@ CASES = {
     "conv3_up_l1_1920": lambda: conv_case(8, 32, 32, 1920, 640, c1=640, residual=True, stats=True),
     "conv3_upsample_320": lambda: conv_case(8, 32, 32, 640, 640, up=True, stats=True),
     "conv3_l2_up_2560": lambda: conv_case(8, 16, 16, 2560, 1280, c1=1280, residual=True, stats=True),
+    "gemm_proj_1280_l2": lambda: conv_case(8, 16, 16, 1280, 1280, k=1, residual=True),
+    "gemm_proj_1280_l3": lambda: conv_case(8, 8, 8, 1280, 1280, k=1, residual=True),
+    "gemm_qkv_1280": lambda: conv_case(8, 16, 16, 1280, 3840, k=1),
+    "gemm_ff2_5120": lambda: conv_case(8, 16, 16, 5120, 1280, k=1, residual=True),
+    "gemm_geglu_1280_l2": lambda: conv_case(8, 16, 16, 1280, 10240, k=1, geglu=True),
+    "conv3_l3_2560": lambda: conv_case(8, 8, 8, 2560, 1280, c1=1280, residual=True, stats=True),
+    "conv3_s2_l2": lambda: conv_case(8, 16, 16, 1280, 1280, stride=2, stats=True),
     "attn_4096_d40": lambda: attn_case(8, 4096, 320),
     "attn_1024_d80": lambda: attn_case(8, 1024, 640),
     "attn_256_d160": lambda: attn_case(8, 256, 1280),
     "gn_l0_fused": lambda: gn_case(8, 4096, 320, True),
     "gn_l0_unfused": lambda: gn_case(8, 4096, 320, False),
     "ln_l0": lambda: ln_case(32768, 320),
+    "ln_l1": lambda: ln_case(8192, 640),
+    "ln_l2": lambda: ln_case(2048, 1280),
 }
 
 

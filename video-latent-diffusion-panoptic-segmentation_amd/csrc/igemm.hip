@@ -46,12 +46,56 @@ struct ConvArgs {
   int ksplit;         // > 1: write fp32 partials to `partial` [ksplit][M][n]
   float* partial;
   float2* gn_part;    // optional [M/64][n] (sum, sumsq) of the final output values
+  int tap_inner;      // K tiles visited channel-block-major, taps inner (see k_state)
 };
 
 constexpr int kBufFlags = 0x00020000;
 constexpr int kOOB = 0x7ffffff0;  // offset past every num_records: the load returns zeros
 
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// Order in which a block visits its K tiles.  Packed K is tap-major (ky, kx, c), but when
+// every tile lies inside one tap (cin % BK == 0) the tiles are visited channel-block-major
+// with the 9 taps innermost: the same 64 input channels of the same input rows are then
+// re-read 9 times within 9 consecutive tiles (an L2 hit) instead of once per tap sweep
+// (which, at the 64x64 level, falls out of the XCD's 4 MB L2 into the Infinity Cache).
+// Per lane: ch = channel of its 16-B chunk, (tap, ky, kx), kofs = packed-K offset.
+struct KState {
+  int ch, tap, ky, kx, kofs;
+  __device__ __forceinline__ void init(const ConvArgs& p, int kt0, int bk, int lane_k) {
+    const int ntaps = p.ksize * p.ksize;
+    if (p.tap_inner) {
+      const int cb = kt0 / ntaps;
+      tap = kt0 - cb * ntaps;
+      ch = cb * bk + lane_k;
+      kofs = tap * p.cin + ch;
+    } else {
+      ch = kt0 * bk + lane_k;
+      kofs = ch;
+      tap = ch / p.cin;
+      ch -= tap * p.cin;
+    }
+    ky = tap / p.ksize;
+    kx = tap - ky * p.ksize;
+  }
+  __device__ __forceinline__ bool valid(const ConvArgs& p) const { return tap < p.ksize * p.ksize && ch < p.cin; }
+  __device__ __forceinline__ void advance(const ConvArgs& p, int bk) {
+    if (p.tap_inner) {
+      ++tap;
+      if (++kx == p.ksize) { kx = 0; ++ky; }
+      if (tap == p.ksize * p.ksize) { tap = 0; ky = 0; kx = 0; ch += bk; }
+      kofs = tap * p.cin + ch;
+    } else {
+      kofs += bk;
+      ch += bk;
+      while (ch >= p.cin) {
+        ch -= p.cin;
+        ++tap;
+        if (++kx == p.ksize) { kx = 0; ++ky; }
+      }
+    }
+  }
+};
 
 __device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
@@ -366,14 +410,13 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   //      wave instruction), so the XOR swizzle moves to the SOURCE: the lane at chunk position cc
   //      of row r fetches logical chunk cc ^ swz(r) (swizzle source + read, never the LDS dest).
   const int cl = DMA ? (cc ^ ((rr >> 1) & 7)) : cc;
-  int ch = kt0 * BK + cl * CE, tap = ch / p.cin;
-  ch -= tap * p.cin;
-  int ky = tap / p.ksize, kx = tap - ky * p.ksize;
-  const int ntaps = p.ksize * p.ksize;
+  KState ks_;
+  ks_.init(p, kt0, BK, cl * CE);
 
   auto a_offset = [&](int i, int cs, int choff, bool kval) -> int {
     int pixel;
     bool ok = rok[i] && kval;
+    const int ky = ks_.ky, kx = ks_.kx;
     if (p.upsample) {
       const int uy = iy0[i] + ky, ux = ix0[i] + kx;
       ok = ok && (unsigned)uy < (unsigned)(2 * p.h_in) && (unsigned)ux < (unsigned)(2 * p.w_in);
@@ -385,18 +428,11 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     }
     return ok ? (pixel * cs + choff) * ES : kOOB;
   };
-  auto b_offset = [&](int i, int kt) -> int {
+  auto b_offset = [&](int i) -> int {
     const int n = n0 + rr + 32 * i;
-    return (n < p.n) ? (n * p.kpad + kt * BK + cl * CE) * ES : kOOB;
+    return (n < p.n) ? (n * p.kpad + ks_.kofs) * ES : kOOB;
   };
-  auto advance = [&]() {
-    ch += BK;
-    while (ch >= p.cin) {
-      ch -= p.cin;
-      ++tap;
-      if (++kx == p.ksize) { kx = 0; ++ky; }
-    }
-  };
+  auto advance = [&]() { ks_.advance(p, BK); };
 
   f32x4_t acc[FM][FN];
 #pragma unroll
@@ -449,7 +485,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     auto issue_dma = [&](int kt, int buf) {
       const unsigned abase = lds0 + (unsigned)(buf * (BM + BN) * 8 * 16);
       const unsigned bbase = abase + BM * 8 * 16;
-      const bool kval = tap < ntaps;
+      const int ch = ks_.ch;
+      const bool kval = ks_.valid(p);
       const int sel = __builtin_amdgcn_readfirstlane((p.c1 > 0 && ch >= p.c0) ? 1 : 0);
       const int cs = sel ? p.c1 : p.c0;
       const int choff = sel ? ch - p.c0 : ch;
@@ -463,7 +500,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
 #pragma unroll
       for (int i = 0; i < BI; ++i) {
         const unsigned dst = __builtin_amdgcn_readfirstlane(bbase + (32 * i + 8 * wv) * 128);
-        dma16(rw, b_offset(i, kt), dst);
+        dma16(rw, b_offset(i), dst);
       }
       advance();
     };
@@ -481,7 +518,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     // ---- register-staged pipeline (per-lane source select for an unaligned concat)
     uint4 va[AI], vb[BI];
     auto issue_loads = [&](int kt) {
-      const bool kval = tap < ntaps;
+      const int ch = ks_.ch;
+      const bool kval = ks_.valid(p);
       const bool lane_src1 = p.c1 > 0 && ch >= p.c0;
       const int cs = lane_src1 ? p.c1 : p.c0;
       const int choff = lane_src1 ? ch - p.c0 : ch;
@@ -494,7 +532,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
         va[i] = make_uint4(x0.x | x1.x, x0.y | x1.y, x0.z | x1.z, x0.w | x1.w);
       }
 #pragma unroll
-      for (int i = 0; i < BI; ++i) vb[i] = bload(rw, b_offset(i, kt));
+      for (int i = 0; i < BI; ++i) vb[i] = bload(rw, b_offset(i));
       advance();
     };
     auto store_lds = [&](int buf) {
@@ -669,10 +707,8 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
   }
   // source-side swizzle: (row >> 1) & 7 is the same for every row this lane loads
   const int cl = cc ^ ((rr >> 1) & 7);
-  int ch = kt0 * BK + cl * CE, tap = ch / p.cin;
-  ch -= tap * p.cin;
-  int ky = tap / p.ksize, kx = tap - ky * p.ksize;
-  const int ntaps = p.ksize * p.ksize;
+  KState ks_;
+  ks_.init(p, kt0, BK, cl * CE);
 
   typedef __attribute__((address_space(3))) uint4 lds_u4_t;
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
@@ -681,7 +717,8 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
   auto issue = [&](int kt, int st) {
     const unsigned abase = lds0 + (unsigned)(st * STAGE_U4 * 16);
     const unsigned bbase = abase + BM * 128;
-    const bool kval = tap < ntaps;
+    const int ch = ks_.ch, ky = ks_.ky, kx = ks_.kx;
+    const bool kval = ks_.valid(p);
     const int sel = __builtin_amdgcn_readfirstlane((p.c1 > 0 && ch >= p.c0) ? 1 : 0);
     const int cs = sel ? p.c1 : p.c0;
     const int choff = sel ? ch - p.c0 : ch;
@@ -703,7 +740,7 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
       if (sel) dma16(ra1, off, dst);
       else dma16(ra0, off, dst);
     }
-    const int kb = (kt * BK + cl * CE) * ES;
+    const int kb = ks_.kofs * ES;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       if (i == 2 && !b_extra) break;
@@ -711,12 +748,7 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
       const int off = n < p.n ? n * p.kpad * ES + kb : kOOB;
       dma16(rw, off, __builtin_amdgcn_readfirstlane(bbase + (64 * i + 8 * wv) * 128));
     }
-    ch += BK;
-    while (ch >= p.cin) {
-      ch -= p.cin;
-      ++tap;
-      if (++kx == p.ksize) { kx = 0; ++ky; }
-    }
+    ks_.advance(p, BK);
   };
 
   f32x4_t acc[FM][FN];
@@ -891,28 +923,53 @@ Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
       return pl;
     }
   }
-  // Large tiles when they alone fill the chip and waste little of N.
-  if (big_ok) {
-    const int tn = (q->n + 159) / 160;
-    const int tiles = ((M + 255) / 256) * tn;
-    if (tiles >= 240 && tn * 160 * 10 <= q->n * 11) {
-      pl.bm = 256; pl.bn = 160; pl.ksplit = 1;
+  // Tuned on the SD UNet shapes at B=8 (tools/opbench.py plan sweeps, profiles/r01_*):
+  //  - large 256x160 tiles for deep K when they fill the chip, split K by 2 when half-full;
+  //  - GEGLU (gelu epilogue): large tiles from K >= 1280, else 128x128;
+  //  - deep K over few tiles (8x8 / 16x16 levels): split K to ~320-640 blocks;
+  //  - shallow 1x1 GEMMs: the smallest tile that still gives >= 400 blocks (occupancy and
+  //    epilogue/prologue overlap beat per-block efficiency at 5-20 K tiles).
+  auto tiles_of = [&](int bm, int bn) { return ((M + bm - 1) / bm) * ((q->n + bn - 1) / bn); };
+  const int tn_big = (q->n + 159) / 160;
+  const bool waste_ok = tn_big * 160 * 10 <= q->n * 11;
+  const int tiles_big = ((M + 255) / 256) * tn_big;
+  pl.ksplit = 1;
+  if (q->out_layout == LDM_OUT_GEGLU) {
+    if (big_ok && waste_ok && nk >= 20 && tiles_big >= 240) { pl.bm = 256; pl.bn = 160; return pl; }
+    pl.bm = M <= 32 ? 32 : (M <= 64 ? 64 : 128);
+    pl.bn = 128;
+    if (tiles_of(pl.bm, 128) < 256) pl.bn = 64;
+    return pl;
+  }
+  if (big_ok && waste_ok && nk >= 40) {
+    if (tiles_big >= 240) { pl.bm = 256; pl.bn = 160; return pl; }
+    if (tiles_big >= 96 && nk >= 64 && split_ok) {
+      pl.bm = 256; pl.bn = 160;
+      pl.ksplit = std::min((256 + tiles_big - 1) / tiles_big, std::min(4, nk / 32));
       return pl;
     }
   }
-  pl.bm = M <= 32 ? 32 : (M <= 64 ? 64 : 128);
-  pl.bn = q->n <= 32 ? 32 : (q->n <= 64 ? 64 : 128);
-  if (q->out_layout == LDM_OUT_GEGLU && pl.bn < 64) pl.bn = 64;
-  pl.ksplit = 1;
-  // Split K when the tile grid cannot fill the chip (the 8x8 / 16x16 UNet levels): aim for
-  // ~2 blocks per CU, keep >= 8 K tiles per split.  Not for GEGLU / pixel-shuffle outputs.
-  const int tiles = ((M + pl.bm - 1) / pl.bm) * ((q->n + pl.bn - 1) / pl.bn);
-  if (split_ok && tiles < 256 && nk >= 16) {
-    int ks = (512 + tiles - 1) / tiles;
-    ks = std::min(ks, nk / 8);
-    ks = std::min(ks, 16);
-    if (ks > 1) pl.ksplit = ks;
+  const int bn_small = q->n <= 32 ? 32 : (q->n <= 64 ? 64 : 128);
+  if (M <= 64) {                     // a handful of rows (time-embedding MLP)
+    pl.bm = M <= 32 ? 32 : 64;
+    pl.bn = std::min(bn_small, 64);
+    return pl;
   }
+  if (nk >= 64 && split_ok && tiles_of(64, bn_small) < 400) {
+    if (M <= 1024) {
+      pl.bm = 128; pl.bn = bn_small;
+      pl.ksplit = std::max(1, std::min((320 + tiles_of(128, pl.bn) - 1) / tiles_of(128, pl.bn), std::min(8, nk / 16)));
+    } else {
+      pl.bm = 64; pl.bn = bn_small;
+      const int t = tiles_of(64, pl.bn);
+      pl.ksplit = std::max(1, std::min((640 + t / 2) / t, nk / 16));
+    }
+    return pl;
+  }
+  if (q->n >= 2048 && tiles_of(128, 128) >= 400) { pl.bm = 128; pl.bn = 128; return pl; }
+  pl.bm = 64;
+  pl.bn = bn_small;
+  if (tiles_of(64, pl.bn) < 400 && pl.bn > 64) pl.bn = 64;
   return pl;
 }
 
@@ -1010,6 +1067,7 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.tiles_n = 0;
   a.nblk = 0;
   a.mixed_src = mixed ? 1 : 0;
+  a.tap_inner = (!mixed && q->ksize > 1 && cin % bk == 0 && q->c0 % bk == 0) ? 1 : 0;
   a.ksplit = pl.ksplit;
   a.partial = static_cast<float*>(q->workspace);
   a.gn_part = reinterpret_cast<float2*>(q->gn_partial);

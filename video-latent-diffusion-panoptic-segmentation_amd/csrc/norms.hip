@@ -9,6 +9,8 @@
 // read in place.
 #include "common.h"
 
+#include <algorithm>
+
 namespace {
 
 constexpr int GN_PPC = 64;  // pixels per partial chunk (== the conv epilogue's 64-row chunks)
@@ -85,86 +87,154 @@ __global__ __launch_bounds__(256) void gn_finalize(const float2* __restrict__ pa
   }
 }
 
+// y = silu?(x * scale[b, c] + shift[b, c]) over 16-byte vectors; each thread takes UNR
+// vectors a grid-stride apart and issues all their loads before any math (HBM latency
+// overlaps), with 32-bit index math (nvec < 2^31 is checked on the host).
 template <typename T>
 __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x0, const T* __restrict__ x1, int c0, int c1,
-                                                int hw, int64_t nvec, const float2* __restrict__ table, int act,
+                                                int hw, int nvec, const float2* __restrict__ table, int act,
                                                 T* __restrict__ out) {
   constexpr int EPC = 16 / sizeof(T);
+  constexpr int UNR = 4;
   const int C = c0 + c1, V = C / EPC;
-  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < nvec; i += (int64_t)gridDim.x * 256) {
-    const int64_t m = i / V;
-    const int v = (int)(i - m * V);
-    const int b = (int)(m / hw);
-    const int c = v * EPC;
-    const uint4 raw = (c < c0) ? *reinterpret_cast<const uint4*>(x0 + m * c0 + c)
-                               : *reinterpret_cast<const uint4*>(x1 + m * c1 + (c - c0));
-    const T* e = reinterpret_cast<const T*>(&raw);
-    const float4* tb = reinterpret_cast<const float4*>(table + (int64_t)b * C + c);
-    uint4 res;
-    T* r = reinterpret_cast<T*>(&res);
+  const int step = gridDim.x * 256;
+  for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < nvec; i0 += UNR * step) {
+    uint4 raw[UNR];
+    int mm[UNR], cc[UNR];
 #pragma unroll
-    for (int k = 0; k < EPC; k += 2) {
-      const float4 st = tb[k >> 1];   // (scale_k, shift_k, scale_k+1, shift_k+1)
-      float y0 = to_f(e[k]) * st.x + st.y;
-      float y1 = to_f(e[k + 1]) * st.z + st.w;
-      if (act == LDM_ACT_SILU) { y0 = silu_f(y0); y1 = silu_f(y1); }
-      r[k] = from_f<T>(y0);
-      r[k + 1] = from_f<T>(y1);
+    for (int u = 0; u < UNR; ++u) {
+      const int i = i0 + u * step;
+      const int m = i / V;
+      const int c = (i - m * V) * EPC;
+      mm[u] = m;
+      cc[u] = c;
+      if (i < nvec)
+        raw[u] = (c < c0) ? *reinterpret_cast<const uint4*>(x0 + (int64_t)m * c0 + c)
+                          : *reinterpret_cast<const uint4*>(x1 + (int64_t)m * c1 + (c - c0));
     }
-    *reinterpret_cast<uint4*>(out + m * C + c) = res;
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      if (i0 + u * step >= nvec) break;
+      const int b = mm[u] / hw, c = cc[u];
+      const T* e = reinterpret_cast<const T*>(&raw[u]);
+      const float4* tb = reinterpret_cast<const float4*>(table + (int64_t)b * C + c);
+      uint4 res;
+      T* r = reinterpret_cast<T*>(&res);
+#pragma unroll
+      for (int k = 0; k < EPC; k += 2) {
+        const float4 st = tb[k >> 1];   // (scale_k, shift_k, scale_k+1, shift_k+1)
+        float y0 = to_f(e[k]) * st.x + st.y;
+        float y1 = to_f(e[k + 1]) * st.z + st.w;
+        if (act == LDM_ACT_SILU) { y0 = silu_f(y0); y1 = silu_f(y1); }
+        r[k] = from_f<T>(y0);
+        r[k + 1] = from_f<T>(y1);
+      }
+      *reinterpret_cast<uint4*>(out + (int64_t)mm[u] * C + c) = res;
+    }
   }
 }
 
-// LayerNorm over the last dim: one wave per row, two-pass (mean, then centred variance) in fp32.
-template <typename T, int MAXV>
+// LayerNorm over the last dim, two-pass (mean, then centred variance) in fp32 registers.
+// G lanes per row (G | 64): a wave normalises 64/G rows at once, each lane holding NV 16-byte
+// chunks (chunk v = lane_in_row + G * i), so C = 320 bf16 (40 chunks) runs 8 rows per wave
+// with every lane busy; reductions are xor-shuffles within the G-lane group.  Grid-stride
+// over row groups.
+template <typename T, int G, int NV>
 __global__ __launch_bounds__(256) void ln_kernel(const T* __restrict__ x, int rows, int C,
                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
                                                  float eps, int act, T* __restrict__ out) {
   constexpr int EPC = 16 / sizeof(T);
+  constexpr int RPW = 64 / G;                      // rows per wave
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= rows) return;
+  const int gl = lane % G;
   const int V = C / EPC;
-  const T* xr = x + (int64_t)row * C;
-  float vals[MAXV][EPC];
-  float s = 0.f;
+  const float inv_c = 1.0f / (float)C;
+  const int stride = gridDim.x * 4 * RPW;
+  for (int row = (blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / G; row - lane / G < rows; row += stride) {
+    const bool rv = row < rows;
+    const T* xr = x + (int64_t)row * C;
+    float vals[NV][EPC];
+    float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int v = lane + 64 * i;
-    if (v < V) {
-      const uint4 raw = *reinterpret_cast<const uint4*>(xr + v * EPC);
-      const T* e = reinterpret_cast<const T*>(&raw);
+    for (int i = 0; i < NV; ++i) {
+      const int v = gl + G * i;
+      if (rv && v < V) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(xr + v * EPC);
+        const T* e = reinterpret_cast<const T*>(&raw);
 #pragma unroll
-      for (int k = 0; k < EPC; ++k) { vals[i][k] = to_f(e[k]); s += vals[i][k]; }
-    }
-  }
-  const float mean = wave_sum(s) / C;
-  float q = 0.f;
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    if (lane + 64 * i < V) {
-#pragma unroll
-      for (int k = 0; k < EPC; ++k) { const float d = vals[i][k] - mean; q += d * d; }
-    }
-  }
-  const float rstd = rsqrtf(wave_sum(q) / C + eps);
-  T* orow = out + (int64_t)row * C;
-#pragma unroll
-  for (int i = 0; i < MAXV; ++i) {
-    const int v = lane + 64 * i;
-    if (v < V) {
-      uint4 res;
-      T* r = reinterpret_cast<T*>(&res);
-#pragma unroll
-      for (int k = 0; k < EPC; ++k) {
-        const int ch = v * EPC + k;
-        float y = (vals[i][k] - mean) * rstd * gamma[ch] + beta[ch];
-        if (act == LDM_ACT_SILU) y = silu_f(y);
-        r[k] = from_f<T>(y);
+        for (int k = 0; k < EPC; ++k) { vals[i][k] = to_f(e[k]); s += vals[i][k]; }
       }
-      *reinterpret_cast<uint4*>(orow + v * EPC) = res;
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s * inv_c;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (rv && gl + G * i < V) {
+#pragma unroll
+        for (int k = 0; k < EPC; ++k) { const float d = vals[i][k] - mean; q += d * d; }
+      }
+    }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = rsqrtf(q * inv_c + eps);
+    T* orow = out + (int64_t)row * C;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = gl + G * i;
+      if (rv && v < V) {
+        float gm[EPC], bt[EPC];
+#pragma unroll
+        for (int k = 0; k < EPC; k += 4) {
+          const float4 g4 = *reinterpret_cast<const float4*>(gamma + v * EPC + k);
+          const float4 b4 = *reinterpret_cast<const float4*>(beta + v * EPC + k);
+          gm[k] = g4.x; gm[k + 1] = g4.y; gm[k + 2] = g4.z; gm[k + 3] = g4.w;
+          bt[k] = b4.x; bt[k + 1] = b4.y; bt[k + 2] = b4.z; bt[k + 3] = b4.w;
+        }
+        uint4 res;
+        T* r = reinterpret_cast<T*>(&res);
+#pragma unroll
+        for (int k = 0; k < EPC; ++k) {
+          float y = (vals[i][k] - mean) * rstd * gm[k] + bt[k];
+          if (act == LDM_ACT_SILU) y = silu_f(y);
+          r[k] = from_f<T>(y);
+        }
+        *reinterpret_cast<uint4*>(orow + v * EPC) = res;
+      }
     }
   }
+}
+
+template <typename T, int G>
+int ln_launch_g(const void* x, int rows, int c, const float* gamma, const float* beta, float eps, int act, void* out,
+                hipStream_t s) {
+  constexpr int EPC = 16 / sizeof(T);
+  const int V = c / EPC;
+  const int nv = (V + G - 1) / G;
+  const int rpb = 4 * (64 / G);
+  const int grid = std::min((rows + rpb - 1) / rpb, 256 * 16);
+#define LN_CASE(NVC)                                                                                       \
+  if (nv <= NVC) {                                                                                         \
+    hipLaunchKernelGGL((ln_kernel<T, G, NVC>), dim3(grid), dim3(256), 0, s, (const T*)x, rows, c, gamma, beta, \
+                       eps, act, (T*)out);                                                                 \
+    return LDM_OK;                                                                                         \
+  }
+  LN_CASE(1) LN_CASE(2) LN_CASE(4) LN_CASE(5) LN_CASE(8) LN_CASE(16)
+#undef LN_CASE
+  return LDM_ERR_ARG;
+}
+
+template <typename T>
+int ln_launch(const void* x, int rows, int c, const float* gamma, const float* beta, float eps, int act, void* out,
+              hipStream_t s) {
+  constexpr int EPC = 16 / sizeof(T);
+  const int V = c / EPC;
+  // the smallest lane group that keeps <= 8 chunks per lane
+  if (V <= 8 * 8) return ln_launch_g<T, 8>(x, rows, c, gamma, beta, eps, act, out, s);
+  if (V <= 16 * 8) return ln_launch_g<T, 16>(x, rows, c, gamma, beta, eps, act, out, s);
+  if (V <= 32 * 8) return ln_launch_g<T, 32>(x, rows, c, gamma, beta, eps, act, out, s);
+  return ln_launch_g<T, 64>(x, rows, c, gamma, beta, eps, act, out, s);
 }
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
@@ -201,9 +271,10 @@ int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw,
                      groups, eps, gamma, beta, table);
   LDM_CHECK_LAUNCH();
   const int64_t nvec = (int64_t)batch * hw * (C / EPC);
-  const int64_t blocks = std::min<int64_t>((nvec + 255) / 256, 256 * 8);
+  if (nvec >= (1LL << 31) - 4 * 256 * 2048) return LDM_ERR_ARG;
+  const int64_t blocks = std::min<int64_t>((nvec + 4 * 256 - 1) / (4 * 256), 256 * 8);
   hipLaunchKernelGGL((gn_apply<T>), dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const T*>(x0),
-                     static_cast<const T*>(x1), c0, c1, hw, nvec, table, act, static_cast<T*>(out));
+                     static_cast<const T*>(x1), c0, c1, hw, (int)nvec, table, act, static_cast<T*>(out));
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
@@ -244,24 +315,11 @@ extern "C" int ldm_layer_norm(const void* x, int rows, int c, const float* gamma
   const int epc = dtype == LDM_F32 ? 4 : 8;
   if (c % epc) return LDM_ERR_ALIGN;
   if (!aligned16(x) || !aligned16(out)) return LDM_ERR_ALIGN;
-  const int V = c / epc;
+  if (!aligned16(gamma) || !aligned16(beta)) return LDM_ERR_ALIGN;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  dim3 grid((rows + 3) / 4);
-  if (dtype == LDM_BF16) {
-    if (V <= 64 * 4) hipLaunchKernelGGL((ln_kernel<bf16_t, 4>), grid, dim3(256), 0, s, (const bf16_t*)x, rows, c,
-                                        gamma, beta, eps, act, (bf16_t*)out);
-    else if (V <= 64 * 8) hipLaunchKernelGGL((ln_kernel<bf16_t, 8>), grid, dim3(256), 0, s, (const bf16_t*)x, rows,
-                                             c, gamma, beta, eps, act, (bf16_t*)out);
-    else return LDM_ERR_ARG;
-  } else {
-    if (V <= 64 * 4) hipLaunchKernelGGL((ln_kernel<float, 4>), grid, dim3(256), 0, s, (const float*)x, rows, c,
-                                        gamma, beta, eps, act, (float*)out);
-    else if (V <= 64 * 8) hipLaunchKernelGGL((ln_kernel<float, 8>), grid, dim3(256), 0, s, (const float*)x, rows, c,
-                                             gamma, beta, eps, act, (float*)out);
-    else if (V <= 64 * 16) hipLaunchKernelGGL((ln_kernel<float, 16>), grid, dim3(256), 0, s, (const float*)x, rows,
-                                              c, gamma, beta, eps, act, (float*)out);
-    else return LDM_ERR_ARG;
-  }
+  const int st = dtype == LDM_BF16 ? ln_launch<bf16_t>(x, rows, c, gamma, beta, eps, act, out, s)
+                                   : ln_launch<float>(x, rows, c, gamma, beta, eps, act, out, s);
+  if (st != LDM_OK) return st;
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
