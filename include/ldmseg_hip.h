@@ -107,6 +107,17 @@ typedef struct {
 } ldm_attn_params;
 
 int ldm_attention(const ldm_attn_params* p, ldm_stream_t stream);
+/* Training forward: as ldm_attention, and also stores lse[(b * heads + h) * n_q + q] =
+ * log2-domain row log-sum-exp of the scaled scores (max2 + log2(l)), consumed by the backward. */
+int ldm_attention_fwd_lse(const ldm_attn_params* p, float* lse, ldm_stream_t stream);
+/* Backward of ldm_attention (the autograd of diffusers Attention's softmax(QK^T s)V that the
+ * reference training step differentiates, trainers_ldm_cond.py:851-856): given o, do and lse,
+ * writes dq/dk/dv (same row layout/strides as q/k/v; may be column slices of one [N][3C]
+ * tensor).  workspace: >= ldm_attention_bwd_workspace_bytes(p) bytes. */
+size_t ldm_attention_bwd_workspace_bytes(const ldm_attn_params* p);
+int ldm_attention_bwd(const ldm_attn_params* p, const void* o, const void* d_o, int do_stride, const float* lse,
+                      void* dq, void* dk, void* dv, int dq_stride, int dkv_stride, void* workspace,
+                      ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_group_norm — GroupNorm (+ optional SiLU) over NHWC rows of one or two channel-
@@ -122,6 +133,11 @@ int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, int batch, in
                    const float* gamma, const float* beta, float eps, int act, void* out,
                    const float* stats0, const float* stats1, void* workspace, int dtype,
                    ldm_stream_t stream);
+/* Training forward: also stores (mean, rstd) per (batch, group) [batch][groups] float2. */
+int ldm_group_norm_ex(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
+                      const float* gamma, const float* beta, float eps, int act, void* out,
+                      const float* stats0, const float* stats1, void* workspace, float* save_mean_rstd,
+                      int dtype, ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_layer_norm — LayerNorm over the channel dimension of [rows][c] (NHWC pixels or tokens).
@@ -202,6 +218,84 @@ enum { LDM_POST_NONE = 0, LDM_POST_TANH = 1, LDM_POST_SIGMOID = 2, LDM_POST_CLIP
 int ldm_gaussian_posterior(const void* moments, int batch, int hw, int latent_channels,
                            int clamp_output, int act_fn, float* mean, float* logvar, float* std,
                            float* var, int dtype, ldm_stream_t stream);
+
+
+/* =======================================================================================
+ * Training path: backward of the fused forward ops and the
+ * optimizer step.  Replaces the torch autograd backward + AdamW of the reference training
+ * step (trainers_ldm_cond.py:792-900: compute_loss :530-619, loss.backward :851-856,
+ * update_weights :769-781 = clip_grad_norm_ + AdamW from trainers/optim.py:53-82).
+ * Gradients of weights / affine params are fp32; activation gradients use the compute dtype.
+ * ======================================================================================= */
+
+/* ldm_conv2d_wgrad — weight gradient of ldm_conv2d: dW[n][k] = sum_m dY[m][n] * A[m][k] with the
+ * same implicit im2col A as the forward (geometry fields as ldm_conv_params; upsample 0/1).
+ * dy: NHWC [batch*h_out*w_out][n] (compute dtype, n % 8 == 0 for bf16).  dw: fp32 in the torch
+ * layout [n][cin_real][ksize][ksize] (ksize 1: [n][cin_real]); geglu: dy columns are the packed
+ * GEGLU interleave and dw rows are written un-interleaved; accumulate: dw += instead of =. */
+typedef struct {
+  const void* a0; const void* a1; int c0, c1;
+  int batch, h_in, w_in, h_out, w_out, ksize, stride, upsample;
+  const void* dy; int n; int kpad;
+  int cin_real, geglu;
+  float* dw; int accumulate;
+  int dtype;
+  void* workspace; int64_t workspace_bytes;
+} ldm_wgrad_params;
+size_t ldm_conv2d_wgrad_workspace_bytes(const ldm_wgrad_params* p);
+int ldm_conv2d_wgrad(const ldm_wgrad_params* p, ldm_stream_t stream);
+
+/* ldm_colsum — out[s][c] (+)= sum over the rows of segment s of x[rows][c] (segments split the
+ * rows evenly).  Bias gradients (1 segment) and per-batch time-embedding gradients (batch
+ * segments).  geglu: columns are the packed GEGLU interleave, out is un-interleaved. fp32 out. */
+int ldm_colsum(const void* x, int rows, int c, int segments, int geglu, float* out, int accumulate, int dtype,
+               ldm_stream_t stream);
+
+/* ldm_group_norm_bwd — backward of ldm_group_norm_ex (act NONE or SILU) given the saved
+ * (mean, rstd).  dx of the two sources goes to dx0 [rows][c0] / dx1 [rows][c1]; acc0/acc1 add
+ * into what they hold; add_src (optional, [rows][c0+c1]) is added too (a parallel branch's
+ * gradient, e.g. a conv_shortcut dgrad).  dgamma/dbeta fp32 [C] (accumulated if acc_params). */
+size_t ldm_group_norm_bwd_workspace_bytes(int batch, int hw, int channels, int groups);
+int ldm_group_norm_bwd(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
+                       const float* mean_rstd, const float* gamma, const float* beta, int act,
+                       const void* dy, const void* add_src, void* dx0, void* dx1, int acc0, int acc1,
+                       float* dgamma, float* dbeta, int acc_params, void* workspace, int dtype,
+                       ldm_stream_t stream);
+
+/* ldm_layer_norm_bwd — LayerNorm backward over [rows][c]; dx = LN'(dy) + add_src (the residual
+ * stream's gradient).  dgamma/dbeta fp32 [c]. */
+int ldm_layer_norm_bwd(const void* x, const void* dy, int rows, int c, const float* gamma, float eps,
+                       const void* add_src, void* dx, float* dgamma, float* dbeta, int acc_params, int dtype,
+                       ldm_stream_t stream);
+
+/* ldm_geglu — diffusers GEGLU on the packed GEMM output hg [rows][2f] ([h16 | g16] blocks):
+ * dout == NULL: out[rows][f] = h * gelu(g);  else dhg[rows][2f] = (dout gelu(g), dout h gelu'(g)). */
+int ldm_geglu(const void* hg, const void* dout, int rows, int f, void* out, void* dhg, int dtype,
+              ldm_stream_t stream);
+
+/* ldm_sum_pool2 — NHWC 2x2 sum pooling [batch][2h][2w][c] -> [batch][h][w][c] (data gradient of
+ * the Upsample2D nearest-2x); accumulate: out +=. */
+int ldm_sum_pool2(const void* x, int batch, int h_out, int w_out, int c, void* out, int accumulate, int dtype,
+                  ldm_stream_t stream);
+
+/* ldm_mse_loss — trainers_ldm_cond.py:592-604 (l2, ohem_ratio 1): per element
+ * l = (pred - target)^2 * mask[b][pix] * weights[t[b]]; *loss_sum = sum l (fp64, device);
+ * dpred = 2 (pred - target) mask w * grad_scale (NULL: loss only).  pred/dpred NCHW in dtype,
+ * target fp32 NCHW, mask fp32 [batch][hw] or NULL, weights fp32 [num_weights] or NULL. */
+int ldm_mse_loss(const void* pred, const float* target, const float* mask, const int64_t* t,
+                 const float* weights, int num_weights, int batch, int ch, int hw, float grad_scale,
+                 void* dpred, double* loss_sum, int dtype, ldm_stream_t stream);
+
+/* ldm_sq_norm — *sum (+)= sum g^2 over a flat fp32 buffer (fp64 accumulation, device). */
+int ldm_sq_norm(const float* g, int64_t n, double* sum, int accumulate, ldm_stream_t stream);
+
+/* ldm_adamw — torch.optim.AdamW step over flat fp32 buffers (param, grad, exp_avg, exp_avg_sq).
+ * segments: device array of {int64 begin, int64 end, float lr, float weight_decay} (24 B each,
+ * sorted, per-parameter hyper-parameters of trainers/optim.py get_optimizer_params);
+ * sqsum (device, may be NULL) + max_norm > 0 applies clip_grad_norm_'s coefficient. */
+int ldm_adamw(float* param, const float* grad, float* exp_avg, float* exp_avg_sq, const void* segments, int nseg,
+              int64_t n, float beta1, float beta2, float eps, int step, const double* sqsum, float max_norm,
+              ldm_stream_t stream);
 
 const char* ldm_status_string(int status);
 int ldm_abi_version(void);

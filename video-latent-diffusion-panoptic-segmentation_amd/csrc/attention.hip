@@ -24,6 +24,7 @@ struct AttnArgs {
   int qs, ks, vs, os;
   int heads, d, nq, nkv;
   float scale_log2;
+  float* lse;         // optional [batch][heads][nq]: log2-domain log-sum-exp (training forward)
 };
 
 __device__ const uint4 kZeros16 = {0u, 0u, 0u, 0u};
@@ -32,21 +33,6 @@ __device__ const uint4 kOnesF32 = {0x3f800000u, 0u, 0u, 0u};    // fp32 1.0 then
 
 constexpr int KVT = 64;        // keys per tile
 constexpr float kRescaleThr = 8.0f;
-
-// 16 B per lane global -> LDS at M0 + 16 * lane (inline asm: see igemm.hip dma16; the
-// consumer waits with an explicit vmcnt + barrier).  Per-lane 64-bit source address.
-__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_addr) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_addr)
-      : "memory");
-}
 
 template <typename T, int DP, int QSUB, bool ONES>
 __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnArgs p) {
@@ -238,6 +224,7 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnArgs p) {
     const float inv = 1.0f / lt;
     const int qi = qbase + 16 * s + lr;
     if (qi >= p.nq) continue;
+    if (p.lse && g == 0) p.lse[((int64_t)b * p.heads + h) * p.nq + qi] = mrun[s] + __log2f(lt);
 #pragma unroll
     for (int dd = 0; dd < ND; ++dd) {
       const int d = 16 * dd + 4 * g;
@@ -288,11 +275,349 @@ int launch_t(const AttnArgs& a, int batch, hipStream_t s) {
   }
 }
 
+
+// ======================================================================================
+// Backward (flash-attention-2 style, P recomputed from the saved log2-domain LSE):
+//   D[q]   = sum_d dO[q][d] O[q][d]
+//   P      = 2^(S c2 - lse2[q]),  dP = dO V^T,  dZ = P (dP - D[q])     (Z = scale Q K^T)
+//   dV = P^T dO,  dK = scale dZ^T Q   (attn_bwd_kv: one block per 64 keys, loop over queries)
+//   dQ = scale dZ K                   (attn_bwd_q : one block per 64 queries, loop over keys)
+// Both loops stage the streamed operand pair (Q, dO) / (K, V) by LDS-DMA exactly like the
+// forward's K/V tiles (double buffered, zero-filled past n and head_dim); the per-wave fixed
+// operands live in registers.  Transposed fragments (dO^T, Q^T, K^T) come from the row-major
+// LDS tiles via ds_read_b64_tr_b16 (bf16) or scalar reads (fp32).
+// ======================================================================================
+struct AttnBwdArgs {
+  const char* q; const char* k; const char* v; const char* o; const char* dout;
+  char* dq; char* dk; char* dv;
+  int qs, ks, vs, os, dos, dqs, dkvs;
+  int heads, d, nq, nkv;
+  float scale, scale_log2;
+  const float* lse;
+  float* dvec;        // D [batch][heads][nq]
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_dot(const AttnBwdArgs p, int batch) {
+  // one 16-lane group per (b, h, q) row: D = sum_d dO * O
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int l = threadIdx.x & 15;
+  const int total = batch * p.heads * p.nq;
+  float s = 0.f;
+  int b = 0, h = 0, qi = 0;
+  if (row < total) {
+    qi = row % p.nq;
+    const int bh = row / p.nq;
+    h = bh % p.heads;
+    b = bh / p.heads;
+    const T* o = reinterpret_cast<const T*>(p.o) + ((int64_t)b * p.nq + qi) * p.os + (int64_t)h * p.d;
+    const T* g = reinterpret_cast<const T*>(p.dout) + ((int64_t)b * p.nq + qi) * p.dos + (int64_t)h * p.d;
+    for (int dd = l; dd < p.d; dd += 16) s += to_f(o[dd]) * to_f(g[dd]);
+  }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) s += __shfl_xor(s, off, 16);
+  if (row < total && l == 0) p.dvec[row] = s;
+}
+
+// A-operand fragment of a TRANSPOSED row-major LDS tile: lane (g, lr) gets tile[r0 + 4g + j][c0 + lr]
+template <typename T, int ROW>
+__device__ __forceinline__ Frag4<T> tr_frag(const T* tile, int r0, int c0, int g, int lr) {
+  Frag4<T> f;
+  if constexpr (sizeof(T) == 2) {
+    typedef __attribute__((ext_vector_type(4))) short s4_t;
+    typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+    const T* addr = tile + (r0 + 4 * g + (lr >> 2)) * ROW + c0 + 4 * (lr & 3);
+    const s4_t x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(addr));
+    f.v = __builtin_bit_cast(uint2, x);
+  } else {
+    float* e = reinterpret_cast<float*>(&f.v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) e[j] = to_f(tile[(r0 + 4 * g + j) * ROW + c0 + lr]);
+  }
+  return f;
+}
+
+template <typename T>
+__device__ __forceinline__ Frag4<T> pack4(const f32x4_t& v) {
+  Frag4<T> f;
+  if constexpr (sizeof(T) == 2) {
+    bf16_t hb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) hb[r] = f2bf(v[r]);
+    f.v = *reinterpret_cast<const uint2*>(hb);
+  } else {
+    float pv[4] = {v[0], v[1], v[2], v[3]};
+    f.v = *reinterpret_cast<const uint4*>(pv);
+  }
+  return f;
+}
+
+// stage rows [r0, r0 + 64) of two [n][stride] operands (head h) into LDS tiles [64][ROW]
+template <typename T, int DP>
+__device__ __forceinline__ void stage_pair(const T* ap, int as, const T* bp, int bs, int n, int dh, int r0,
+                                           unsigned abase, unsigned bbase, int wave, int lane) {
+  constexpr int EPC = 16 / sizeof(T), CPR = DP / EPC, RCH = CPR + 1;
+  for (int i = wave; i < RCH; i += 4) {
+    const int L = i * 64 + lane;
+    const int row = L / RCH, c = L - row * RCH;
+    const int r = r0 + row, dd = c * EPC;
+    const bool ok = r < n && c < CPR && dd < dh;
+    const void* sa = ok ? (const void*)(ap + (int64_t)r * as + dd) : (const void*)&kZeros16;
+    const void* sb = ok ? (const void*)(bp + (int64_t)r * bs + dd) : (const void*)&kZeros16;
+    const unsigned off = __builtin_amdgcn_readfirstlane(i * 64 * 16);
+    glds16(sa, abase + off);
+    glds16(sb, bbase + off);
+  }
+}
+
+template <typename T, int DP>
+__global__ __launch_bounds__(256, (sizeof(T) == 2 && DP <= 80) ? 2 : 1) void attn_bwd_kv(const AttnBwdArgs p) {
+  constexpr int ES = sizeof(T), EPC = 16 / ES, ND = DP / 16;
+  constexpr int CPR = DP / EPC, RCH = CPR + 1, ROW = RCH * EPC, TILE = KVT * ROW;
+  constexpr int NBUF = (2 * 2 * TILE * ES <= 96 * 1024) ? 2 : 1;   // fp32 at large d: single buffer
+  __shared__ uint4 smem[NBUF * 2 * TILE * ES / 16];
+  T* const lds = reinterpret_cast<T*>(smem);
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, g = lane >> 4;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int kv = blockIdx.x * 64 + wave * 16 + lr;       // this lane's key (B-operand column)
+  const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
+  const T* dop = reinterpret_cast<const T*>(p.dout) + (int64_t)b * p.nq * p.dos + (int64_t)h * p.d;
+  const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
+  const T* vp = reinterpret_cast<const T*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * p.d;
+  const float* lse = p.lse + ((int64_t)b * p.heads + h) * p.nq;
+  const float* dv = p.dvec + ((int64_t)b * p.heads + h) * p.nq;
+
+  Frag4<T> kf[ND], vf[ND];                 // B operands: K^T / V^T columns = this lane's key
+#pragma unroll
+  for (int ds = 0; ds < ND; ++ds) {
+    const int dd = 16 * ds + 4 * g;
+    if (kv < p.nkv && dd < p.d) {
+      kf[ds] = *reinterpret_cast<const Frag4<T>*>(kp + (int64_t)kv * p.ks + dd);
+      vf[ds] = *reinterpret_cast<const Frag4<T>*>(vp + (int64_t)kv * p.vs + dd);
+    } else {
+      kf[ds] = Frag4<T>{};
+      vf[ds] = Frag4<T>{};
+    }
+  }
+  f32x4_t dkt[ND], dvt[ND];                // [d = 16 dd + 4g + r][key = lr]
+#pragma unroll
+  for (int i = 0; i < ND; ++i) { dkt[i] = f32x4_t{0.f, 0.f, 0.f, 0.f}; dvt[i] = f32x4_t{0.f, 0.f, 0.f, 0.f}; }
+  const float c2 = p.scale_log2;
+
+  auto compute = [&](int buf, int q0) {
+    const T* Qs = lds + buf * 2 * TILE;
+    const T* Ds = Qs + TILE;
+#pragma unroll
+    for (int qs = 0; qs < 4; ++qs) {
+      // S[q][key] and dP[q][key]: rows q = qs*16 + 4g + r
+      f32x4_t s = f32x4_t{0.f, 0.f, 0.f, 0.f}, dp = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < ND; ++ds) {
+        const Frag4<T> qa = *reinterpret_cast<const Frag4<T>*>(Qs + (16 * qs + lr) * ROW + 16 * ds + 4 * g);
+        const Frag4<T> da = *reinterpret_cast<const Frag4<T>*>(Ds + (16 * qs + lr) * ROW + 16 * ds + 4 * g);
+        mma_k16(s, qa, kf[ds]);
+        mma_k16(dp, da, vf[ds]);
+      }
+      f32x4_t pm, dz;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qi = q0 + 16 * qs + 4 * g + r;
+        const bool ok = qi < p.nq && kv < p.nkv;
+        const float pr = ok ? __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse[qi])) : 0.f;
+        pm[r] = pr;
+        dz[r] = ok ? pr * (dp[r] - dv[qi]) : 0.f;
+      }
+      const Frag4<T> pf = pack4<T>(pm), zf = pack4<T>(dz);
+#pragma unroll
+      for (int dd = 0; dd < ND; ++dd) {
+        mma_k16(dvt[dd], tr_frag<T, ROW>(Ds, 16 * qs, 16 * dd, g, lr), pf);   // dV^T += dO^T P
+        mma_k16(dkt[dd], tr_frag<T, ROW>(Qs, 16 * qs, 16 * dd, g, lr), zf);   // dK^T += Q^T dZ
+      }
+    }
+  };
+
+  const int ntiles = (p.nq + KVT - 1) / KVT;
+  stage_pair<T, DP>(qp, p.qs, dop, p.dos, p.nq, p.d, 0, lds0, lds0 + TILE * ES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = NBUF == 2 ? (t & 1) : 0;
+    if (NBUF == 2 && t + 1 < ntiles) {
+      const unsigned nb = lds0 + (unsigned)((buf ^ 1) * 2 * TILE * ES);
+      stage_pair<T, DP>(qp, p.qs, dop, p.dos, p.nq, p.d, (t + 1) * KVT, nb, nb + TILE * ES, wave, lane);
+    }
+    compute(buf, t * KVT);
+    if (NBUF == 1 && t + 1 < ntiles) {
+      __syncthreads();
+      stage_pair<T, DP>(qp, p.qs, dop, p.dos, p.nq, p.d, (t + 1) * KVT, lds0, lds0 + TILE * ES, wave, lane);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (kv >= p.nkv) return;
+  T* dkp = reinterpret_cast<T*>(p.dk) + ((int64_t)b * p.nkv + kv) * p.dkvs + (int64_t)h * p.d;
+  T* dvp = reinterpret_cast<T*>(p.dv) + ((int64_t)b * p.nkv + kv) * p.dkvs + (int64_t)h * p.d;
+#pragma unroll
+  for (int dd = 0; dd < ND; ++dd) {
+    const int d0 = 16 * dd + 4 * g;
+    if (d0 >= p.d) continue;
+    float kk[4], vv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { kk[r] = dkt[dd][r] * p.scale; vv[r] = dvt[dd][r]; }
+    if constexpr (ES == 2) {
+      bf16_t hk[4], hv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { hk[r] = f2bf(kk[r]); hv[r] = f2bf(vv[r]); }
+      *reinterpret_cast<uint2*>(dkp + d0) = *reinterpret_cast<const uint2*>(hk);
+      *reinterpret_cast<uint2*>(dvp + d0) = *reinterpret_cast<const uint2*>(hv);
+    } else {
+      *reinterpret_cast<float4*>(dkp + d0) = make_float4(kk[0], kk[1], kk[2], kk[3]);
+      *reinterpret_cast<float4*>(dvp + d0) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    }
+  }
+}
+
+template <typename T, int DP>
+__global__ __launch_bounds__(256, (sizeof(T) == 2 && DP <= 80) ? 2 : 1) void attn_bwd_q(const AttnBwdArgs p) {
+  constexpr int ES = sizeof(T), EPC = 16 / ES, ND = DP / 16;
+  constexpr int CPR = DP / EPC, RCH = CPR + 1, ROW = RCH * EPC, TILE = KVT * ROW;
+  constexpr int NBUF = (2 * 2 * TILE * ES <= 96 * 1024) ? 2 : 1;   // fp32 at large d: single buffer
+  __shared__ uint4 smem[NBUF * 2 * TILE * ES / 16];
+  T* const lds = reinterpret_cast<T*>(smem);
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, g = lane >> 4;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int qi = blockIdx.x * 64 + wave * 16 + lr;       // this lane's query (B-operand column)
+  const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
+  const T* dop = reinterpret_cast<const T*>(p.dout) + (int64_t)b * p.nq * p.dos + (int64_t)h * p.d;
+  const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
+  const T* vp = reinterpret_cast<const T*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * p.d;
+  const bool qok = qi < p.nq;
+  const float lse_q = qok ? p.lse[((int64_t)b * p.heads + h) * p.nq + qi] : 0.f;
+  const float d_q = qok ? p.dvec[((int64_t)b * p.heads + h) * p.nq + qi] : 0.f;
+
+  Frag4<T> qf[ND], gf[ND];
+#pragma unroll
+  for (int ds = 0; ds < ND; ++ds) {
+    const int dd = 16 * ds + 4 * g;
+    if (qok && dd < p.d) {
+      qf[ds] = *reinterpret_cast<const Frag4<T>*>(qp + (int64_t)qi * p.qs + dd);
+      gf[ds] = *reinterpret_cast<const Frag4<T>*>(dop + (int64_t)qi * p.dos + dd);
+    } else {
+      qf[ds] = Frag4<T>{};
+      gf[ds] = Frag4<T>{};
+    }
+  }
+  f32x4_t dqt[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) dqt[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const float c2 = p.scale_log2;
+
+  auto compute = [&](int buf, int k0) {
+    const T* Ks = lds + buf * 2 * TILE;
+    const T* Vs = Ks + TILE;
+#pragma unroll
+    for (int js = 0; js < 4; ++js) {
+      // S^T[key][q], dP^T[key][q]: rows key = js*16 + 4g + r, column q = lr
+      f32x4_t s = f32x4_t{0.f, 0.f, 0.f, 0.f}, dp = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ds = 0; ds < ND; ++ds) {
+        const Frag4<T> ka = *reinterpret_cast<const Frag4<T>*>(Ks + (16 * js + lr) * ROW + 16 * ds + 4 * g);
+        const Frag4<T> va = *reinterpret_cast<const Frag4<T>*>(Vs + (16 * js + lr) * ROW + 16 * ds + 4 * g);
+        mma_k16(s, ka, qf[ds]);
+        mma_k16(dp, va, gf[ds]);
+      }
+      f32x4_t dz;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = k0 + 16 * js + 4 * g + r;
+        const bool ok = qok && kj < p.nkv;
+        const float pr = ok ? __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse_q)) : 0.f;
+        dz[r] = pr * (dp[r] - d_q);
+      }
+      const Frag4<T> zf = pack4<T>(dz);
+#pragma unroll
+      for (int dd = 0; dd < ND; ++dd) mma_k16(dqt[dd], tr_frag<T, ROW>(Ks, 16 * js, 16 * dd, g, lr), zf);  // dQ^T += K^T dZ^T
+    }
+  };
+
+  const int ntiles = (p.nkv + KVT - 1) / KVT;
+  stage_pair<T, DP>(kp, p.ks, vp, p.vs, p.nkv, p.d, 0, lds0, lds0 + TILE * ES, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = NBUF == 2 ? (t & 1) : 0;
+    if (NBUF == 2 && t + 1 < ntiles) {
+      const unsigned nb = lds0 + (unsigned)((buf ^ 1) * 2 * TILE * ES);
+      stage_pair<T, DP>(kp, p.ks, vp, p.vs, p.nkv, p.d, (t + 1) * KVT, nb, nb + TILE * ES, wave, lane);
+    }
+    compute(buf, t * KVT);
+    if (NBUF == 1 && t + 1 < ntiles) {
+      __syncthreads();
+      stage_pair<T, DP>(kp, p.ks, vp, p.vs, p.nkv, p.d, (t + 1) * KVT, lds0, lds0 + TILE * ES, wave, lane);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (!qok) return;
+  T* dqp = reinterpret_cast<T*>(p.dq) + ((int64_t)b * p.nq + qi) * p.dqs + (int64_t)h * p.d;
+#pragma unroll
+  for (int dd = 0; dd < ND; ++dd) {
+    const int d0 = 16 * dd + 4 * g;
+    if (d0 >= p.d) continue;
+    float qq[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) qq[r] = dqt[dd][r] * p.scale;
+    if constexpr (ES == 2) {
+      bf16_t hq[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hq[r] = f2bf(qq[r]);
+      *reinterpret_cast<uint2*>(dqp + d0) = *reinterpret_cast<const uint2*>(hq);
+    } else {
+      *reinterpret_cast<float4*>(dqp + d0) = make_float4(qq[0], qq[1], qq[2], qq[3]);
+    }
+  }
+}
+
+template <typename T, int DP>
+int launch_bwd_dp(const AttnBwdArgs& a, int batch, hipStream_t s) {
+  hipLaunchKernelGGL((attn_bwd_kv<T, DP>), dim3((a.nkv + 63) / 64, a.heads, batch), dim3(256), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  hipLaunchKernelGGL((attn_bwd_q<T, DP>), dim3((a.nq + 63) / 64, a.heads, batch), dim3(256), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+template <typename T>
+int launch_bwd(const AttnBwdArgs& a, int batch, hipStream_t s) {
+  const int rows = batch * a.heads * a.nq;
+  hipLaunchKernelGGL(attn_bwd_dot<T>, dim3((rows + 15) / 16), dim3(256), 0, s, a, batch);
+  LDM_CHECK_LAUNCH();
+  const int dp = (a.d + 15) / 16 * 16;
+  switch (dp) {
+    case 16: return launch_bwd_dp<T, 16>(a, batch, s);
+    case 32: return launch_bwd_dp<T, 32>(a, batch, s);
+    case 48: return launch_bwd_dp<T, 48>(a, batch, s);
+    case 64: return launch_bwd_dp<T, 64>(a, batch, s);
+    case 80: return launch_bwd_dp<T, 80>(a, batch, s);
+    case 96: return launch_bwd_dp<T, 96>(a, batch, s);
+    case 128: return launch_bwd_dp<T, 128>(a, batch, s);
+    case 160: return launch_bwd_dp<T, 160>(a, batch, s);
+    default: return LDM_ERR_ARG;
+  }
+}
+
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 }  // namespace
 
-extern "C" int ldm_attention(const ldm_attn_params* q, ldm_stream_t stream) {
+namespace {
+int attn_validate(const ldm_attn_params* q) {
   if (!q || !q->q || !q->k || !q->v || !q->o) return LDM_ERR_ARG;
   if (q->dtype != LDM_F32 && q->dtype != LDM_BF16) return LDM_ERR_ARG;
   if (q->batch <= 0 || q->heads <= 0 || q->n_q <= 0 || q->n_kv <= 0) return LDM_ERR_ARG;
@@ -301,6 +626,10 @@ extern "C" int ldm_attention(const ldm_attn_params* q, ldm_stream_t stream) {
   const int ce = 16 / es;
   if (q->k_stride % ce || q->v_stride % ce || q->q_stride % 4 || q->o_stride % 4) return LDM_ERR_ALIGN;
   if (!aligned16(q->k) || !aligned16(q->v) || !aligned16(q->q) || !aligned16(q->o)) return LDM_ERR_ALIGN;
+  return LDM_OK;
+}
+
+AttnArgs attn_args(const ldm_attn_params* q) {
   AttnArgs a;
   a.q = static_cast<const char*>(q->q);
   a.k = static_cast<const char*>(q->k);
@@ -309,6 +638,61 @@ extern "C" int ldm_attention(const ldm_attn_params* q, ldm_stream_t stream) {
   a.qs = q->q_stride; a.ks = q->k_stride; a.vs = q->v_stride; a.os = q->o_stride;
   a.heads = q->heads; a.d = q->head_dim; a.nq = q->n_q; a.nkv = q->n_kv;
   a.scale_log2 = q->scale * 1.4426950408889634f;
+  a.lse = nullptr;
+  return a;
+}
+}  // namespace
+
+extern "C" int ldm_attention(const ldm_attn_params* q, ldm_stream_t stream) {
+  const int st = attn_validate(q);
+  if (st != LDM_OK) return st;
+  const AttnArgs a = attn_args(q);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, q->batch, s) : launch_t<float>(a, q->batch, s);
+}
+
+extern "C" int ldm_attention_fwd_lse(const ldm_attn_params* q, float* lse, ldm_stream_t stream) {
+  const int st = attn_validate(q);
+  if (st != LDM_OK) return st;
+  if (!lse) return LDM_ERR_ARG;
+  AttnArgs a = attn_args(q);
+  a.lse = lse;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, q->batch, s) : launch_t<float>(a, q->batch, s);
+}
+
+extern "C" size_t ldm_attention_bwd_workspace_bytes(const ldm_attn_params* q) {
+  if (!q || q->batch <= 0 || q->heads <= 0 || q->n_q <= 0) return 0;
+  return ((size_t)q->batch * q->heads * q->n_q * sizeof(float) + 15) & ~(size_t)15;
+}
+
+extern "C" int ldm_attention_bwd(const ldm_attn_params* q, const void* o, const void* d_o, int do_stride,
+                                 const float* lse, void* dq, void* dk, void* dv, int dq_stride, int dkv_stride,
+                                 void* workspace, ldm_stream_t stream) {
+  const int st = attn_validate(q);
+  if (st != LDM_OK) return st;
+  if (!o || !d_o || !lse || !dq || !dk || !dv || !workspace) return LDM_ERR_ARG;
+  if (do_stride % 4 || dq_stride % 4 || dkv_stride % 4) return LDM_ERR_ALIGN;
+  if (!aligned16(d_o) || !aligned16(workspace)) return LDM_ERR_ALIGN;
+  const int es = q->dtype == LDM_F32 ? 4 : 2;
+  const int ce = 16 / es;
+  if (q->q_stride % ce || do_stride % ce) return LDM_ERR_ALIGN;   // Q / dO tiles are DMA-staged too
+  AttnBwdArgs a;
+  a.q = static_cast<const char*>(q->q);
+  a.k = static_cast<const char*>(q->k);
+  a.v = static_cast<const char*>(q->v);
+  a.o = static_cast<const char*>(o);
+  a.dout = static_cast<const char*>(d_o);
+  a.dq = static_cast<char*>(dq);
+  a.dk = static_cast<char*>(dk);
+  a.dv = static_cast<char*>(dv);
+  a.qs = q->q_stride; a.ks = q->k_stride; a.vs = q->v_stride; a.os = q->o_stride;
+  a.dos = do_stride; a.dqs = dq_stride; a.dkvs = dkv_stride;
+  a.heads = q->heads; a.d = q->head_dim; a.nq = q->n_q; a.nkv = q->n_kv;
+  a.scale = q->scale;
+  a.scale_log2 = q->scale * 1.4426950408889634f;
+  a.lse = lse;
+  a.dvec = static_cast<float*>(workspace);
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  return q->dtype == LDM_BF16 ? launch_bwd<bf16_t>(a, q->batch, s) : launch_bwd<float>(a, q->batch, s);
 }

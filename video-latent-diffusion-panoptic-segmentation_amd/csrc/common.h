@@ -104,6 +104,22 @@ __device__ __forceinline__ void mma_k16(f32x4_t& acc, const Frag4<float>& a, con
   for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[j], pb[j], acc, 0, 0, 0);
 }
 
+// 16 B per lane global -> LDS at M0 + 16 * lane (LDS-DMA, per-lane 64-bit source).
+// Inline asm so that hipcc does not drain every in-flight DMA before the next ds_read; the
+// consumer owns the wait (explicit `s_waitcnt vmcnt` + barrier).  M0 is saved and restored.
+__device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_addr)
+      : "memory");
+}
+
 #define LDM_CHECK_LAUNCH()                                   \
   do {                                                       \
     hipError_t _e = hipGetLastError();                       \

@@ -2,7 +2,9 @@
 //
 // One kernel covers every matmul-shaped op of the denoising path: 3x3 convs (stride 1/2,
 // optional nearest-2x upsampled input, optional two-source channel concat), 1x1 convs /
-// linears, and the ConvTranspose k2s2 of the seg-VAE decoder (pixel-shuffle epilogue).
+// linears, the stride-2 data gradient (a 3x3 conv over the zero-inserted output gradient:
+// `upsample == 2` reads the input as if dilated x2 with zeros between samples), and the
+// ConvTranspose k2s2 of the seg-VAE decoder (pixel-shuffle epilogue).
 //   rows m = output pixels (b, oy, ox) of NHWC activations
 //   cols n = output channels; weights pre-packed [n][kpad], K contiguous
 //   k      = (ky, kx, c) tap-major, consumed in K tiles of 128 bytes
@@ -420,6 +422,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     if (p.upsample) {
       const int uy = iy0[i] + ky, ux = ix0[i] + kx;
       ok = ok && (unsigned)uy < (unsigned)(2 * p.h_in) && (unsigned)ux < (unsigned)(2 * p.w_in);
+      if (p.upsample == 2) ok = ok && !((uy | ux) & 1);    // zero-inserted (dilated) input
       pixel = (pix0[i] + (uy >> 1)) * p.w_in + (ux >> 1);
     } else {
       const int iy = iy0[i] + ky, ix = ix0[i] + kx;
@@ -729,6 +732,7 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
       if (p.upsample) {
         const int uy = iy0[i] + ky, ux = ix0[i] + kx;
         ok = ok && (unsigned)uy < (unsigned)(2 * p.h_in) && (unsigned)ux < (unsigned)(2 * p.w_in);
+        if (p.upsample == 2) ok = ok && !((uy | ux) & 1);
         pixel = (pix0[i] + (uy >> 1)) * p.w_in + (ux >> 1);
       } else {
         const int iy = iy0[i] + ky, ix = ix0[i] + kx;
@@ -980,7 +984,7 @@ int validate(const ldm_conv_params* q, int* es_out) {
   const int ce = 16 / es;
   if (q->ksize != 1 && q->ksize != 3) return LDM_ERR_ARG;
   if (q->stride != 1 && q->stride != 2) return LDM_ERR_ARG;
-  if (q->upsample && (q->stride != 1)) return LDM_ERR_ARG;
+  if (q->upsample < 0 || q->upsample > 2 || (q->upsample && (q->stride != 1))) return LDM_ERR_ARG;
   if (q->batch <= 0 || q->h_in <= 0 || q->w_in <= 0 || q->h_out <= 0 || q->w_out <= 0) return LDM_ERR_ARG;
   if (q->c0 <= 0 || q->c1 < 0 || (q->c1 > 0 && !q->a1)) return LDM_ERR_ARG;
   if (q->c0 % ce || q->c1 % ce) return LDM_ERR_ALIGN;

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void gn_partial(const T* __restrict__ x, int C
 __global__ __launch_bounds__(256) void gn_finalize(const float2* __restrict__ part0, const float2* __restrict__ part1,
                                                    int c0, int c1, int hw, int chunks, int groups, float eps,
                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                   float2* __restrict__ table) {
+                                                   float2* __restrict__ table, float2* __restrict__ save) {
   const int b = blockIdx.x;
   const int gi = blockIdx.y * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -80,6 +80,7 @@ __global__ __launch_bounds__(256) void gn_finalize(const float2* __restrict__ pa
   double var = q / cnt - mean * mean;
   if (var < 0.0) var = 0.0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  if (save && lane == 0) save[(int64_t)b * groups + gi] = make_float2((float)mean, rstd);   // for the backward
   for (int k = lane; k < cpg; k += 64) {
     const int c = gi * cpg + k;
     const float sc = rstd * gamma[c];
@@ -243,7 +244,7 @@ inline size_t round16(size_t x) { return (x + 15) & ~(size_t)15; }
 template <typename T>
 int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups, const float* gamma,
               const float* beta, float eps, int act, void* out, const float* p0, const float* p1, void* ws,
-              hipStream_t s) {
+              float* save, hipStream_t s) {
   constexpr int EPC = 16 / sizeof(T);
   const int C = c0 + c1;
   const int chunks = (hw + GN_PPC - 1) / GN_PPC;
@@ -268,7 +269,7 @@ int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw,
     part1 = dst;
   }
   hipLaunchKernelGGL(gn_finalize, dim3(batch, (groups + 3) / 4), dim3(256), 0, s, part0, part1, c0, c1, hw, chunks,
-                     groups, eps, gamma, beta, table);
+                     groups, eps, gamma, beta, table, reinterpret_cast<float2*>(save));
   LDM_CHECK_LAUNCH();
   const int64_t nvec = (int64_t)batch * hw * (C / EPC);
   if (nvec >= (1LL << 31) - 4 * 256 * 2048) return LDM_ERR_ARG;
@@ -287,10 +288,10 @@ extern "C" size_t ldm_group_norm_workspace_bytes(int batch, int hw, int channels
                                                                           sizeof(float2)) + 64;
 }
 
-extern "C" int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
-                              const float* gamma, const float* beta, float eps, int act, void* out,
-                              const float* stats0, const float* stats1, void* workspace, int dtype,
-                              ldm_stream_t stream) {
+extern "C" int ldm_group_norm_ex(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
+                                 const float* gamma, const float* beta, float eps, int act, void* out,
+                                 const float* stats0, const float* stats1, void* workspace, float* save_mean_rstd,
+                                 int dtype, ldm_stream_t stream) {
   if (!x0 || !out || !workspace || !gamma || !beta) return LDM_ERR_ARG;
   if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
   if (batch <= 0 || hw <= 0 || c0 <= 0 || c1 < 0 || (c1 > 0 && !x1) || groups <= 0) return LDM_ERR_ARG;
@@ -303,9 +304,17 @@ extern "C" int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, in
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (dtype == LDM_BF16)
     return gn_launch<bf16_t>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1,
-                             workspace, s);
+                             workspace, save_mean_rstd, s);
   return gn_launch<float>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1, workspace,
-                          s);
+                          save_mean_rstd, s);
+}
+
+extern "C" int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
+                              const float* gamma, const float* beta, float eps, int act, void* out,
+                              const float* stats0, const float* stats1, void* workspace, int dtype,
+                              ldm_stream_t stream) {
+  return ldm_group_norm_ex(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1, workspace,
+                           nullptr, dtype, stream);
 }
 
 extern "C" int ldm_layer_norm(const void* x, int rows, int c, const float* gamma, const float* beta, float eps,

@@ -238,6 +238,7 @@ class UNet(nn.Module):
         self.gradient_checkpointing = False
         self._plan = None
         self._plan_key = None
+        self._dplan = None
 
     # ------------------------------------------------------------ diffusers-style API
     @property
@@ -408,8 +409,51 @@ class UNet(nn.Module):
                 P[id(m)] = K.PackedConv(m.conv.weight, m.conv.bias, dt)
         P["out_norm"] = (f32(self.conv_norm_out.weight), f32(self.conv_norm_out.bias))
         P["conv_out"] = K.PackedConv(self.conv_out.weight, self.conv_out.bias, dt)
+        P["resnets"] = resnets
         self._plan, self._plan_key = P, key
+        self._dplan = None
         return P
+
+    def prepare_dgrad(self):
+        """Packed weights of the backward: the data-gradient (transposed, flipped) weight of every
+        conv / linear, keyed by id(module), plus conv_out padded to 8 output channels for its
+        weight gradient (the 4-channel output gradient is padded to 8 for 16-byte rows)."""
+        P = self.prepare()
+        if self._dplan is not None:
+            return self._dplan
+        from .unet_train import packed_dgrad
+        dt = self.dtype
+        D = {}
+        for r in P["resnets"]:
+            D[id(r.conv1)] = packed_dgrad(r.conv1.weight, dt)
+            D[id(r.conv2)] = packed_dgrad(r.conv2.weight, dt)
+            if r.conv_shortcut is not None:
+                D[id(r.conv_shortcut)] = packed_dgrad(r.conv_shortcut.weight, dt)
+        for t in [m for m in self.modules() if isinstance(m, Transformer2DModel)]:
+            tb = t.transformer_blocks[0]
+            a1 = tb.attn1
+            D[id(t.proj_in)] = packed_dgrad(t.proj_in.weight, dt)
+            D[id(t.proj_out)] = packed_dgrad(t.proj_out.weight, dt)
+            D[id(a1)] = packed_dgrad(torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight]), dt)
+            D[id(a1.to_out[0])] = packed_dgrad(a1.to_out[0].weight, dt)
+            D[id(tb.ff.net[0].proj)] = packed_dgrad(tb.ff.net[0].proj.weight, dt, geglu=True)
+            D[id(tb.ff.net[2])] = packed_dgrad(tb.ff.net[2].weight, dt)
+        for m in self.modules():
+            if isinstance(m, (Downsample2D, Upsample2D)):
+                D[id(m)] = packed_dgrad(m.conv.weight, dt)
+        co = self.conv_out.out_channels
+        D["conv_out"] = packed_dgrad(self.conv_out.weight, dt, cin_pad=8)
+        wpad = torch.zeros(8, *self.conv_out.weight.shape[1:], dtype=self.conv_out.weight.dtype,
+                           device=self.conv_out.weight.device)
+        wpad[:co] = self.conv_out.weight.detach()
+        P["conv_out_t"] = K.PackedConv(wpad, None, dt)
+        self._dplan = D
+        return D
+
+    def invalidate_packed(self):
+        """Drop the packed weights (call after an in-place optimizer update that bypasses
+        torch's version counter, e.g. the fused AdamW of ldmseg.trainers)."""
+        self._plan = self._plan_key = self._dplan = None
 
     # ------------------------------------------------------------ HIP forward pieces
     def _resnet(self, P, r, xs, B, H, W, temb_all):
@@ -450,7 +494,9 @@ class UNet(nn.Module):
         h = K.linear(p["ff2"], f, residual=h, out=h)
         return K.conv2d(p["proj_out"], h, B, H, W, residual=x, gn_stats=True)
 
-    @torch.no_grad()
+    def _trainable(self):
+        return [p for p in self.parameters() if p.requires_grad]
+
     def forward(
         self,
         sample: torch.FloatTensor,
@@ -469,7 +515,10 @@ class UNet(nn.Module):
             raise NotImplementedError("class_labels / timestep_cond / attention_mask are not on the reference path")
         if down_block_additional_residuals is not None or mid_block_additional_residual is not None:
             raise NotImplementedError("additional residuals belong to the separate_encoder variant")
-        out = self.forward_sources([sample], timestep, encoder_hidden_states)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            out = _UNetTrainFn.apply(self, timestep, sample, *self._trainable())
+        else:
+            out = self.forward_sources([sample], timestep, encoder_hidden_states)
         if not return_dict:
             return (out,)
         return UNetOutput(sample=out)
@@ -527,6 +576,42 @@ class UNet(nn.Module):
         x = K.group_norm(x, B, H * W, self.conv_norm_out.num_groups, *P["out_norm"], self.conv_norm_out.eps,
                          K.ACT_SILU)
         return K.conv2d(P["conv_out"], x, B, H, W, out_layout=K.OUT_NCHW)
+
+
+class _UNetTrainFn(torch.autograd.Function):
+    """Autograd node of one UNet forward (the drop-in path for the reference's
+    ``loss.backward()``, trainers_ldm_cond.py:851-856): forward on the HIP kernels keeping the
+    activations the hand-written backward (unet_train.UNetTrainGraph) needs; backward returns
+    fp32 gradients for every trainable parameter."""
+
+    @staticmethod
+    def forward(ctx, unet, timestep, sample, *params):
+        from .unet_train import UNetTrainGraph
+        grads = {}
+
+        def sink(p):
+            g = grads.get(p)
+            if g is None:
+                g = grads[p] = torch.empty(p.shape, dtype=torch.float32, device=p.device)
+                return g, False
+            return g, True
+
+        with torch.no_grad():
+            graph = UNetTrainGraph(unet, sink)
+            out = graph.forward([sample.detach()], timestep)
+        ctx.graph, ctx.grads, ctx.params = graph, grads, params
+        return out
+
+    @staticmethod
+    def backward(ctx, d_out):
+        with torch.no_grad():
+            ctx.graph.backward(d_out.to(ctx.graph.u.dtype).contiguous())
+        gs = []
+        for p in ctx.params:
+            g = ctx.grads.get(p)
+            gs.append(None if g is None else g.to(p.dtype))
+        ctx.graph = None
+        return (None, None, None, *gs)
 
 
 def _remap_legacy_keys(sd):

@@ -41,6 +41,13 @@ class AttnParams(ctypes.Structure):
                 ("n_q", _i), ("n_kv", _i), ("scale", _f), ("dtype", _i)]
 
 
+class WgradParams(ctypes.Structure):
+    _fields_ = [("a0", _vp), ("a1", _vp), ("c0", _i), ("c1", _i), ("batch", _i), ("h_in", _i), ("w_in", _i),
+                ("h_out", _i), ("w_out", _i), ("ksize", _i), ("stride", _i), ("upsample", _i), ("dy", _vp),
+                ("n", _i), ("kpad", _i), ("cin_real", _i), ("geglu", _i), ("dw", _vp), ("accumulate", _i),
+                ("dtype", _i), ("workspace", _vp), ("workspace_bytes", _i64)]
+
+
 class DdimParams(ctypes.Structure):
     _fields_ = [("model_output", _vp), ("mo_dtype", _i), ("sample", _vp), ("x_dtype", _i), ("prev", _vp),
                 ("x0", _vp), ("out_dtype", _i), ("n", _i64), ("t", _vp), ("alphas_cumprod", _vp),
@@ -65,6 +72,22 @@ EXPORTS = {
     "ldm_nchw_to_nhwc": (_i, [_vp, _i, _i, _vp, _i, _i, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp]),
     "ldm_resize_bilinear": (_i, [_vp, _i, _i, _i, _i, _i, _f, _f, _f, _f, _vp, _i, _i, _vp]),
     "ldm_gaussian_posterior": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
+    "ldm_attention_fwd_lse": (_i, [ctypes.POINTER(AttnParams), _vp, _vp]),
+    "ldm_attention_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
+    "ldm_attention_bwd": (_i, [ctypes.POINTER(AttnParams), _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
+    "ldm_group_norm_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    "ldm_conv2d_wgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(WgradParams)]),
+    "ldm_conv2d_wgrad": (_i, [ctypes.POINTER(WgradParams), _vp]),
+    "ldm_colsum": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp]),
+    "ldm_group_norm_bwd_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i]),
+    "ldm_group_norm_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp,
+                                _vp, _i, _vp, _i, _vp]),
+    "ldm_layer_norm_bwd": (_i, [_vp, _vp, _i, _i, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp]),
+    "ldm_geglu": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp]),
+    "ldm_sum_pool2": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp]),
+    "ldm_mse_loss": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp]),
+    "ldm_sq_norm": (_i, [_vp, _i64, _vp, _i, _vp]),
+    "ldm_adamw": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i64, _f, _f, _f, _i, _vp, _f, _vp]),
     "ldm_status_string": (ctypes.c_char_p, [_i]),
     "ldm_abi_version": (_i, []),
 }
@@ -541,3 +564,249 @@ def gaussian_posterior(moments, clamp_output, act_fn):
                                       *[_ptr(o) for o in outs], dtype_code(moments.dtype), _stream(moments)),
            "ldm_gaussian_posterior")
     return tuple(outs)
+
+
+# ======================================================================================
+# training path (backward kernels + optimizer)
+# ======================================================================================
+def conv2d_wgrad(pc: PackedConv, x0, batch, h, w, dy, *, x1=None, stride=1, upsample=False, dw=None,
+                 accumulate=False):
+    """Weight gradient of conv2d(pc, x0[, x1]) given dy (NHWC [batch, ho, wo, n], compute dtype).
+
+    Returns dw fp32 in the TORCH layout of the packed weight's source ([n][cin_real][k][k] or
+    [n][cin_real] for 1x1), GEGLU rows un-interleaved.  dw may be a preallocated view."""
+    lib = load_library()
+    _gpu(x0, x1, dy, dw)
+    for t, nm in ((x0, "x0"), (x1, "x1"), (dy, "dy")):
+        _contig(t, nm)
+    if pc.shuffle2:
+        raise NotImplementedError("ConvTranspose weight gradient is not on the UNet training path")
+    c0 = x0.numel() // (batch * h * w)
+    c1 = 0 if x1 is None else x1.numel() // (batch * h * w)
+    if c0 + c1 != pc.cin:
+        raise ValueError(f"wgrad expects {pc.cin} input channels, got {c0}+{c1}")
+    if pc.ksize == 1:
+        ho, wo = h, w
+    elif upsample:
+        ho, wo = 2 * h, 2 * w
+    else:
+        ho, wo = (h + 2 - 3) // stride + 1, (w + 2 - 3) // stride + 1
+    n = pc.n
+    if dy.numel() != batch * ho * wo * n or dy.dtype != pc.dtype or x0.dtype != pc.dtype:
+        raise ValueError("dy must be [batch, ho, wo, n] in the compute dtype")
+    shape = (n, pc.cin_real) if pc.ksize == 1 else (n, pc.cin_real, pc.ksize, pc.ksize)
+    if dw is None:
+        dw = torch.empty(shape, dtype=torch.float32, device=x0.device)
+        accumulate = False
+    elif dw.numel() != math.prod(shape) or dw.dtype != torch.float32 or not dw.is_contiguous():
+        raise ValueError("dw must be a contiguous fp32 tensor of the weight's size")
+    p = WgradParams(_ptr(x0), _ptr(x1), c0, c1, batch, h, w, ho, wo, pc.ksize, stride, int(upsample), _ptr(dy), n,
+                    pc.kpad, pc.cin_real, int(pc.geglu), _ptr(dw), int(accumulate), dtype_code(pc.dtype), None, 0)
+    ws_bytes = int(lib.ldm_conv2d_wgrad_workspace_bytes(ctypes.byref(p)))
+    if ws_bytes == 0:
+        raise ValueError("ldm_conv2d_wgrad rejected the configuration")
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x0.device)
+    p.workspace, p.workspace_bytes = _ptr(ws), ws_bytes
+    ev = _prof_start()
+    _check(lib.ldm_conv2d_wgrad(ctypes.byref(p), _stream(x0)), "ldm_conv2d_wgrad")
+    _prof_stop(ev, "wgrad", 2.0 * batch * ho * wo * n * pc.ksize * pc.ksize * pc.cin_real,
+               (x0.numel() + (0 if x1 is None else x1.numel()) + dy.numel()) * x0.element_size() + ws_bytes * 2,
+               f"k{pc.ksize} M={batch * ho * wo} N={n} Cin={c0}+{c1}")
+    return dw
+
+
+def colsum(x, rows, c, segments=1, geglu=False, out=None, accumulate=False):
+    """fp32 [segments, c] column sums of x viewed as [rows, c]."""
+    lib = load_library()
+    _gpu(x, out)
+    _contig(x, "x")
+    if x.numel() != rows * c:
+        raise ValueError("colsum: numel != rows * c")
+    if out is None:
+        out = torch.empty(segments, c, dtype=torch.float32, device=x.device)
+        accumulate = False
+    elif out.numel() != segments * c or out.dtype != torch.float32 or not out.is_contiguous():
+        raise ValueError("colsum: bad out")
+    _check(lib.ldm_colsum(_ptr(x), rows, c, segments, int(geglu), _ptr(out), int(accumulate), dtype_code(x.dtype),
+                          _stream(x)), "ldm_colsum")
+    return out
+
+
+def group_norm_train(x0, batch, hw, groups, gamma, beta, eps, act=ACT_NONE, x1=None):
+    """group_norm() that also returns the per-(batch, group) (mean, rstd) for the backward."""
+    lib = load_library()
+    _gpu(x0, x1, gamma, beta)
+    _contig(x0, "x0")
+    _contig(x1, "x1")
+    c0 = x0.numel() // (batch * hw)
+    c1 = 0 if x1 is None else x1.numel() // (batch * hw)
+    C = c0 + c1
+    out = torch.empty(batch, hw, C, dtype=x0.dtype, device=x0.device)
+    mr = torch.empty(batch, groups, 2, dtype=torch.float32, device=x0.device)
+    ws = torch.empty(int(lib.ldm_group_norm_workspace_bytes(batch, hw, C)), dtype=torch.uint8, device=x0.device)
+    s0, s1 = gn_stats_of(x0), gn_stats_of(x1)
+    if hw % 64:
+        s0 = s1 = None
+    _check(lib.ldm_group_norm_ex(_ptr(x0), _ptr(x1), c0, c1, batch, hw, groups, _ptr(gamma), _ptr(beta), float(eps),
+                                 act, _ptr(out), _ptr(s0), _ptr(s1), _ptr(ws), _ptr(mr), dtype_code(x0.dtype),
+                                 _stream(x0)), "ldm_group_norm_ex")
+    return out, mr
+
+
+def group_norm_bwd(x0, batch, hw, groups, mean_rstd, gamma, beta, act, dy, *, x1=None, add_src=None, dx0=None,
+                   dx1=None, acc0=False, acc1=False, dgamma=None, dbeta=None, acc_params=False):
+    lib = load_library()
+    _gpu(x0, x1, dy, add_src, dx0, dx1)
+    for t, nm in ((x0, "x0"), (x1, "x1"), (dy, "dy"), (add_src, "add_src")):
+        _contig(t, nm)
+    c0 = x0.numel() // (batch * hw)
+    c1 = 0 if x1 is None else x1.numel() // (batch * hw)
+    C = c0 + c1
+    if dy.numel() != batch * hw * C or dy.dtype != x0.dtype:
+        raise ValueError("group_norm_bwd: dy must be [batch, hw, c0 + c1] in the compute dtype")
+    if dx0 is None:
+        dx0, acc0 = torch.empty_like(x0), False
+    if c1 and dx1 is None:
+        dx1, acc1 = torch.empty_like(x1), False
+    ws = torch.empty(int(lib.ldm_group_norm_bwd_workspace_bytes(batch, hw, C, groups)), dtype=torch.uint8,
+                     device=x0.device)
+    _check(lib.ldm_group_norm_bwd(_ptr(x0), _ptr(x1), c0, c1, batch, hw, groups, _ptr(mean_rstd), _ptr(gamma),
+                                  _ptr(beta), act, _ptr(dy), _ptr(add_src), _ptr(dx0), _ptr(dx1), int(acc0), int(acc1),
+                                  _ptr(dgamma), _ptr(dbeta), int(acc_params), _ptr(ws), dtype_code(x0.dtype),
+                                  _stream(x0)), "ldm_group_norm_bwd")
+    return dx0, dx1
+
+
+def layer_norm_bwd(x, dy, gamma, eps, add_src=None, dx=None, dgamma=None, dbeta=None, acc_params=False):
+    lib = load_library()
+    _gpu(x, dy, add_src, dx)
+    for t, nm in ((x, "x"), (dy, "dy"), (add_src, "add_src")):
+        _contig(t, nm)
+    C = x.shape[-1]
+    rows = x.numel() // C
+    if dx is None:
+        dx = torch.empty_like(x)
+    _check(lib.ldm_layer_norm_bwd(_ptr(x), _ptr(dy), rows, C, _ptr(gamma), float(eps), _ptr(add_src), _ptr(dx),
+                                  _ptr(dgamma), _ptr(dbeta), int(acc_params), dtype_code(x.dtype), _stream(x)),
+           "ldm_layer_norm_bwd")
+    return dx
+
+
+def geglu_fwd(hg):
+    """[..., 2F] packed GEGLU pre-activation -> [..., F] h * gelu(g)."""
+    lib = load_library()
+    _gpu(hg)
+    _contig(hg, "hg")
+    F2 = hg.shape[-1]
+    rows = hg.numel() // F2
+    out = torch.empty(*hg.shape[:-1], F2 // 2, dtype=hg.dtype, device=hg.device)
+    _check(lib.ldm_geglu(_ptr(hg), None, rows, F2 // 2, _ptr(out), None, dtype_code(hg.dtype), _stream(hg)),
+           "ldm_geglu")
+    return out
+
+
+def geglu_bwd(hg, dout):
+    lib = load_library()
+    _gpu(hg, dout)
+    _contig(hg, "hg")
+    _contig(dout, "dout")
+    F2 = hg.shape[-1]
+    rows = hg.numel() // F2
+    dhg = torch.empty_like(hg)
+    _check(lib.ldm_geglu(_ptr(hg), _ptr(dout), rows, F2 // 2, None, _ptr(dhg), dtype_code(hg.dtype), _stream(hg)),
+           "ldm_geglu")
+    return dhg
+
+
+def sum_pool2(x, batch, h_out, w_out, out=None, accumulate=False):
+    lib = load_library()
+    _gpu(x, out)
+    _contig(x, "x")
+    C = x.numel() // (batch * 4 * h_out * w_out)
+    if out is None:
+        out = torch.empty(batch, h_out, w_out, C, dtype=x.dtype, device=x.device)
+        accumulate = False
+    _check(lib.ldm_sum_pool2(_ptr(x), batch, h_out, w_out, C, _ptr(out), int(accumulate), dtype_code(x.dtype),
+                             _stream(x)), "ldm_sum_pool2")
+    return out
+
+
+def mse_loss(pred, target, mask=None, t=None, weights=None, grad_scale=1.0, want_grad=True):
+    """Returns (loss_sum fp64 device scalar, dpred or None)."""
+    lib = load_library()
+    _gpu(pred, target, mask, t, weights)
+    pred = pred.contiguous()
+    target = target.float().contiguous()
+    B, Cc, H, W = pred.shape
+    if mask is not None:
+        mask = mask.float().contiguous()
+        if mask.numel() != B * H * W:
+            raise ValueError("mask must be [B, H, W]")
+    if weights is not None:
+        if t is None or t.dtype != torch.int64 or t.numel() != B:
+            raise ValueError("per-sample int64 timesteps are needed with weights")
+        weights = weights.float().contiguous()
+    dpred = torch.empty_like(pred) if want_grad else None
+    total = torch.empty((), dtype=torch.float64, device=pred.device)
+    _check(lib.ldm_mse_loss(_ptr(pred), _ptr(target), _ptr(mask), _ptr(t), _ptr(weights),
+                            0 if weights is None else weights.numel(), B, Cc, H * W, float(grad_scale), _ptr(dpred),
+                            _ptr(total), dtype_code(pred.dtype), _stream(pred)), "ldm_mse_loss")
+    return total, dpred
+
+
+def sq_norm(g, out=None, accumulate=False):
+    lib = load_library()
+    _gpu(g)
+    if g.dtype != torch.float32 or not g.is_contiguous():
+        raise ValueError("sq_norm takes a contiguous fp32 buffer")
+    if out is None:
+        out = torch.empty((), dtype=torch.float64, device=g.device)
+        accumulate = False
+    _check(lib.ldm_sq_norm(_ptr(g), g.numel(), _ptr(out), int(accumulate), _stream(g)), "ldm_sq_norm")
+    return out
+
+
+def adamw(param, grad, exp_avg, exp_avg_sq, segments, nseg, step, beta1=0.9, beta2=0.999, eps=1e-8, sqsum=None,
+          max_norm=0.0):
+    """segments: device byte tensor of nseg packed {int64 begin, end; float lr, wd} records."""
+    lib = load_library()
+    _gpu(param, grad, exp_avg, exp_avg_sq, segments, sqsum)
+    n = param.numel()
+    for t in (grad, exp_avg, exp_avg_sq):
+        if t.numel() != n or t.dtype != torch.float32:
+            raise ValueError("adamw buffers must be fp32 of equal size")
+    _check(lib.ldm_adamw(_ptr(param), _ptr(grad), _ptr(exp_avg), _ptr(exp_avg_sq), _ptr(segments), int(nseg), n,
+                         float(beta1), float(beta2), float(eps), int(step), _ptr(sqsum), float(max_norm),
+                         _stream(param)), "ldm_adamw")
+
+
+def attention_fwd_lse(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_stride, scale=None):
+    """attention() that also returns the log2-domain LSE [batch, heads, n_q] for the backward."""
+    lib = load_library()
+    _gpu(q, k, v)
+    C = heads * head_dim
+    out = torch.empty(batch, n_q, C, dtype=q.dtype, device=q.device)
+    lse = torch.empty(batch, heads, n_q, dtype=torch.float32, device=q.device)
+    p = AttnParams(_ptr(q), _ptr(k), _ptr(v), _ptr(out), q_stride, k_stride, v_stride, C, batch, heads, head_dim,
+                   n_q, n_kv, float(scale if scale is not None else head_dim ** -0.5), dtype_code(q.dtype))
+    ev = _prof_start()
+    _check(lib.ldm_attention_fwd_lse(ctypes.byref(p), _ptr(lse), _stream(q)), "ldm_attention_fwd_lse")
+    _prof_stop(ev, "attention", 4.0 * batch * heads * n_q * n_kv * head_dim,
+               (2 * batch * n_q * C + 2 * batch * n_kv * C) * q.element_size(), f"N={n_q} L={n_kv} d={head_dim}")
+    return out, lse
+
+
+def attention_bwd(q, k, v, o, d_o, lse, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_stride, dq, dk, dv,
+                  dq_stride, dkv_stride, scale=None):
+    lib = load_library()
+    _gpu(q, k, v, o, d_o, lse, dq, dk, dv)
+    _contig(d_o, "d_o")
+    C = heads * head_dim
+    p = AttnParams(_ptr(q), _ptr(k), _ptr(v), _ptr(o), q_stride, k_stride, v_stride, C, batch, heads, head_dim,
+                   n_q, n_kv, float(scale if scale is not None else head_dim ** -0.5), dtype_code(q.dtype))
+    ws = torch.empty(int(lib.ldm_attention_bwd_workspace_bytes(ctypes.byref(p))), dtype=torch.uint8, device=q.device)
+    ev = _prof_start()
+    _check(lib.ldm_attention_bwd(ctypes.byref(p), _ptr(o), _ptr(d_o), C, _ptr(lse), _ptr(dq), _ptr(dk), _ptr(dv),
+                                 dq_stride, dkv_stride, _ptr(ws), _stream(q)), "ldm_attention_bwd")
+    _prof_stop(ev, "attention_bwd", 10.0 * batch * heads * n_q * n_kv * head_dim,
+               (4 * batch * n_q * C + 4 * batch * n_kv * C) * q.element_size(), f"N={n_q} L={n_kv} d={head_dim}")
