@@ -151,7 +151,12 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=2)
+    ap.add_argument("--mode", default="denoise", choices=["denoise", "train"],
+                    help="denoise: the headline metric; train: config 3's DDP training iteration")
+    ap.add_argument("--clips", type=int, default=2, help="train mode: clips of T frames per GPU")
     args = ap.parse_args()
+    if args.mode == "train":
+        return main_train(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -206,6 +211,80 @@ def main():
             "outputs_finite": finite,
             "roofline": rl,
             "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+TRAIN_METRIC = "LDM training iterations/sec (2 clips x T=8 per GPU, 4x64x64 latents, self-conditioning)"
+
+
+def main_train(args):
+    """BASELINE config 3 (tools/main_ldm.py + train_diffusion.sh): per GPU 2 clips x T=8 = 16
+    frames of [x_t || rgb || self-cond] (12x64x64), SD-1.4 UNet with fp32 master weights
+    computing in bf16 (the reference: fp32 weights + fp16 autocast), self-conditioning forward,
+    SNR-weighted masked L2, hand-written backward, grad clip 1.0, AdamW (lr 1e-4, wd 0.05).
+    N > 1: one process per GPU, gradients summed by bucketed RCCL all-reduces overlapped with
+    the backward (ldmseg/trainers/ddp.py).  value = N x steps / max-over-ranks time."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from ldmseg.models import UNet
+    from ldmseg.schedulers import DDIMNoiseScheduler
+    from ldmseg.trainers import LDMTrainStep
+    from ldmseg.utils import max_over_ranks
+    torch.manual_seed(0)                                   # identical init on every rank (DDP broadcast)
+    with torch.device(dev):
+        u = UNet()
+    u.remove_cross_attention()
+    u.modify_encoder(in_channels=8, init_mode_seg="copy", init_mode_image="zero", cond_channels=4,
+                     init_mode_cond="zero")                 # train_diffusion.sh: self_condition, cond_channels 4
+    u.freeze_layers(["time_embedding"])
+    u.train()
+    sched = DDIMNoiseScheduler(prediction_type="epsilon", beta_schedule="scaled_linear", beta_start=0.00085,
+                               beta_end=0.012, steps_offset=1, clip_sample=False, set_alpha_to_one=False,
+                               weight="max_clamp_snr", max_snr=2.0, device=dev, verbose=False)
+    step = LDMTrainStep(u, sched, lr=1e-4, weight_decay=0.05, clip_grad=1.0, self_condition=True,
+                        compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32, seed=1 + rank)
+    B, L = args.clips * args.frames, args.latent
+    g = torch.Generator().manual_seed(100 + rank)
+    lat = (torch.randn(B, 4, L, L, generator=g)).to(dev)
+    rgb = (torch.randn(B, 4, L, L, generator=g)).to(dev)
+    mask = (torch.rand(B, L, L, generator=g) > 0.05).float().to(dev)
+    for _ in range(args.warmup):
+        step.train_step(lat, rgb, mask)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        loss = step.train_step(lat, rgb, mask)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
+    lv = float(loss.item())
+    if rank == 0:
+        tflop = 4 * 6.17 * B / 8          # fwd + bwd (2x fwd) + self-cond fwd; 6.17 TFLOP per 8-frame fwd
+        line = {
+            "metric": TRAIN_METRIC, "value": round(world * args.steps / elapsed, 4), "unit": "iterations/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic: random-init SD-1.4 UNet weights, N(0,1) latents, 5% ignore mask",
+            "config": {"workload": f"train iteration: self-cond fwd + fwd + bwd + clip + AdamW, {B} frames/GPU",
+                       "model": "SD-1.4 UNet2DConditionModel, cross-attn removed, 12-ch conv_in (815.5M)",
+                       "global_batch": B * world, "seq_len": L * L,
+                       "parallelism": f"dp{world} (RCCL bucketed all-reduce overlapped with backward)"},
+            "loss": round(lv, 6),
+            "algorithmic_tflop_per_iter_per_gpu": round(tflop, 2),
+            "achieved_tflops_per_gpu": round(tflop * args.steps / elapsed, 1),
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -239,11 +239,23 @@ class UNet(nn.Module):
         self._plan = None
         self._plan_key = None
         self._dplan = None
+        self._compute_dtype = None
 
     # ------------------------------------------------------------ diffusers-style API
     @property
     def dtype(self) -> torch.dtype:
         return next(self.parameters()).dtype
+
+    @property
+    def compute_dtype(self) -> torch.dtype:
+        """dtype the HIP kernels compute in: the parameters' dtype, unless set_compute_dtype()
+        chose another (fp32 master weights computing in bf16 — the role of the reference's
+        fp16 autocast, trainers_ldm_cond.py:831,836)."""
+        return self._compute_dtype or self.dtype
+
+    def set_compute_dtype(self, dtype=None):
+        self._compute_dtype = dtype
+        self._plan = self._plan_key = self._dplan = None
 
     @property
     def device(self) -> torch.device:
@@ -349,14 +361,14 @@ class UNet(nn.Module):
 
     # ------------------------------------------------------------ packed-weight plan
     def _signature(self):
-        return (self.dtype, self.device) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+        return (self.compute_dtype, self.device) + tuple((p.data_ptr(), p._version) for p in self.parameters())
 
     def prepare(self, force=False):
         """(Re)pack every weight for the HIP kernels; cached until a parameter changes."""
         key = self._signature()
         if not force and self._plan is not None and self._plan_key == key:
             return self._plan
-        dt = self.dtype
+        dt = self.compute_dtype
         if dt not in (torch.float32, torch.bfloat16):
             raise TypeError(f"UNet HIP path runs in float32 or bfloat16, not {dt}")
         f32 = lambda t: None if t is None else t.detach().float().contiguous()  # noqa: E731
@@ -422,7 +434,7 @@ class UNet(nn.Module):
         if self._dplan is not None:
             return self._dplan
         from .unet_train import packed_dgrad
-        dt = self.dtype
+        dt = self.compute_dtype
         D = {}
         for r in P["resnets"]:
             D[id(r.conv1)] = packed_dgrad(r.conv1.weight, dt)
@@ -484,7 +496,7 @@ class UNet(nn.Module):
             q2 = p["attn2"]
             n = K.layer_norm(h, *q2["ln2"], 1e-5)
             q = K.linear(q2["q"], n)
-            e = ehs.to(self.dtype).contiguous()
+            e = ehs.to(self.compute_dtype).contiguous()
             kv = K.linear(q2["kv"], e)                                   # [B, L, 2C]
             L = e.shape[1]
             a = K.attention(q, kv, kv[..., C:], B, heads, dh, N, L, C, 2 * C, 2 * C)
@@ -529,7 +541,7 @@ class UNet(nn.Module):
         materialising it (the sampler's ``torch.cat([x_t, rgb, cond], 1)``,
         trainers_ldm_cond.py:1134-1141, is folded into the NCHW->NHWC gather of conv_in)."""
         P = self.prepare()
-        dt = self.dtype
+        dt = self.compute_dtype
         sample = sources[0]
         dev = sample.device
         B, _, H, W = sample.shape
@@ -605,7 +617,7 @@ class _UNetTrainFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_out):
         with torch.no_grad():
-            ctx.graph.backward(d_out.to(ctx.graph.u.dtype).contiguous())
+            ctx.graph.backward(d_out.to(ctx.graph.u.compute_dtype).contiguous())
         gs = []
         for p in ctx.params:
             g = ctx.grads.get(p)

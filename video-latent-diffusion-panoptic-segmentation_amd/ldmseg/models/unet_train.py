@@ -145,7 +145,7 @@ class UNetTrainGraph:
         if any(p.requires_grad for p in u.time_embedding.parameters()):
             raise NotImplementedError("a trainable time_embedding is not supported on the native training path "
                                       "(the reference freezes it: freeze_layers ['time_embedding'])")
-        dt = u.dtype
+        dt = u.compute_dtype
         sample = sources[0]
         dev = sample.device
         B, _, H, W = sample.shape
@@ -300,7 +300,7 @@ class UNetTrainGraph:
         u, P = self.u, self.P
         self.dev = d_out_nchw.device
         self.dtemb_parts = {}
-        dt = u.dtype
+        dt = u.compute_dtype
         for kind, m, s in reversed(self.saved):
             if kind == "out":
                 B, H, W = s["B"], s["H"], s["W"]
@@ -364,7 +364,7 @@ class UNetTrainGraph:
         dtemb = torch.zeros(self.B, total, dtype=torch.float32, device=self.dev)
         for off, part in self.dtemb_parts.items():
             dtemb[:, off:off + part.shape[1]] = part
-        dy = dtemb.to(u.dtype).contiguous()
+        dy = dtemb.to(u.compute_dtype).contiguous()
         wt = K.conv2d_wgrad(P["temb_proj"], self.semb, self.B, 1, 1, dy)        # [total, 1280] fp32
         bt = K.colsum(dtemb, self.B, total).view(-1)
         for r in resnets:

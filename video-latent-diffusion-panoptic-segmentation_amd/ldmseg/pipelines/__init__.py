@@ -46,10 +46,7 @@ class DenoiseStep:
                 self.prev, self.x0 = self._body()
 
     def _body(self):
-        dt = self.unet.dtype
-        srcs = [self.lat, self.rgb] + ([self.cond] if self.cond is not None else [])
-        if dt != torch.float32:
-            srcs = [s if s.dtype == dt else s for s in srcs]     # the conv_in gather casts per source
+        srcs = [self.lat, self.rgb] + ([self.cond] if self.cond is not None else [])   # conv_in gather casts
         eps = self.unet.forward_sources(srcs, self.t_f)
         r = self.sched.step(eps, self.t_int, self.lat)
         return r.prev_sample, r.pred_original_sample

@@ -1,0 +1,161 @@
+"""One LDM training iteration on the HIP path (SURVEY.md §8 row a15, row f1 for N > 1).
+
+Follows TrainerDiffusion.train_single_epoch for one batch with gradient_accumulate_every = 1
+(trainers_ldm_cond.py:792-900):
+  noise = randn_like(latents); t = randint(min_noise_level, T, (B,))              :816-821
+  noisy = scheduler.add_noise(latents, noise, t)                                   :822
+  self_condition: cond = remove_noise(noisy, unet([noisy || rgb || 0], t), t)      :824-833 (no grad)
+  compute_loss: pred = unet([noisy || rgb (|| cond)], t); target = noise (epsilon) or latents
+                loss = mean((pred - target)^2 * mask * weights[t])                 :530-619 (l2, ohem 1)
+  loss.backward(); clip_grad_norm_(clip_grad); AdamW step; zero_grad                :851-862, :769-781
+with the optimizer of trainers/optim.py get_optim_unet: per-parameter lr = base_lr *
+lr_factor_func(name), weight decay = weight_decay_norm for norm layers, else weight_decay.
+
+Native pieces: the concatenations are never materialised (the conv_in gather reads the
+sources), the forward keeps activations for the hand-written backward (models/unet_train.py),
+the loss and its gradient are one kernel, the clip coefficient is computed on the device, and
+AdamW is one fused kernel over the flat fp32 master buffer — no host synchronisation inside
+the step.  With torch.distributed initialised, gradients are summed by bucketed all-reduces
+that start while the backward is still running (trainers/ddp.py); the loss gradient carries
+the 1/world factor so the sum is DDP's average.
+
+Not native (raises): ohem_ratio < 1, rgb/cond noise levels > 0, inpainting masks,
+prob_train_on_pred > 0 — all off in base.yaml / train_diffusion.sh.
+"""
+import struct
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from ..models.unet import ResnetBlock2D
+from ..models.unet_train import UNetTrainGraph
+from ..ops import native as K
+from .ddp import FlatParams, GradBucketer
+
+NORM_TYPES = (nn.GroupNorm, nn.LayerNorm, nn.BatchNorm2d)
+
+
+def unet_backward_order(unet):
+    """Trainable parameters in the order the native backward finishes them: reverse forward
+    order of the blocks, every ResNet's time_emb_proj last (its batched GEMM backward runs
+    after the whole graph)."""
+    fwd = [unet.conv_in]
+    for blk in unet.down_blocks:
+        for j, r in enumerate(blk.resnets):
+            fwd.append(r)
+            if blk.has_cross_attention:
+                fwd.append(blk.attentions[j])
+        if blk.downsamplers is not None:
+            fwd.append(blk.downsamplers[0])
+    mb = unet.mid_block
+    fwd += [mb.resnets[0], mb.attentions[0], mb.resnets[1]]
+    for blk in unet.up_blocks:
+        for j, r in enumerate(blk.resnets):
+            fwd.append(r)
+            if blk.has_cross_attention:
+                fwd.append(blk.attentions[j])
+        if blk.upsamplers is not None:
+            fwd.append(blk.upsamplers[0])
+    fwd += [unet.conv_norm_out, unet.conv_out]
+    temb = [q for m in unet.modules() if isinstance(m, ResnetBlock2D) for q in m.time_emb_proj.parameters()]
+    temb_ids = {id(q) for q in temb}
+    order, seen = [], set()
+    for m in reversed(fwd):
+        for q in m.parameters():
+            if q.requires_grad and id(q) not in temb_ids and id(q) not in seen:
+                order.append(q)
+                seen.add(id(q))
+    order += [q for q in temb if q.requires_grad]
+    rest = [q for q in unet.parameters() if q.requires_grad and id(q) not in seen and id(q) not in temb_ids]
+    return order + rest
+
+
+class LDMTrainStep:
+    def __init__(self, unet, scheduler, lr=1e-4, weight_decay=0.0, weight_decay_norm=0.0, betas=(0.9, 0.999),
+                 eps=1e-8, clip_grad=3.0, lr_factor_func=None, self_condition=False, min_noise_level=0,
+                 compute_dtype=torch.bfloat16, bucket_mb=100, group=None, seed=None):
+        self.unet, self.sched = unet, scheduler
+        self.self_condition = self_condition
+        self.min_noise_level = min_noise_level
+        self.clip_grad = float(clip_grad)
+        self.betas, self.eps = betas, eps
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        unet.set_compute_dtype(compute_dtype)
+        names = {id(p): n for n, p in unet.named_parameters()}
+        norm_ids = {id(q) for m in unet.modules() if isinstance(m, NORM_TYPES) for q in m.parameters(recurse=False)}
+        order = unet_backward_order(unet)
+        dev = order[0].device
+        self.flat = FlatParams(order, dev)
+        self.bucketer = GradBucketer(self.flat, bucket_mb * 2 ** 20, group)
+        lr_factor_func = lr_factor_func or unet.get_lr_func
+        self.base_lr = lr
+        self.seg_hp = []
+        for p, o in zip(self.flat.params, self.flat.offsets):
+            plr = lr * lr_factor_func(names[id(p)])
+            wd = weight_decay_norm if id(p) in norm_ids else weight_decay
+            self.seg_hp.append([o, o + p.numel(), plr, wd])
+        self._upload_segments()
+        self.exp_avg = torch.zeros_like(self.flat.data)
+        self.exp_avg_sq = torch.zeros_like(self.flat.data)
+        self.step_count = 0
+        self.sqsum = torch.zeros((), dtype=torch.float64, device=dev)
+        self.gen = None
+        if seed is not None:
+            self.gen = torch.Generator(device=dev)
+            self.gen.manual_seed(seed)
+        unet.invalidate_packed()
+
+    def _upload_segments(self):
+        recs = b"".join(struct.pack("<qqff", s, e, lr, wd) for s, e, lr, wd in self.seg_hp)
+        self.segs = torch.frombuffer(bytearray(recs), dtype=torch.uint8).to(self.flat.data.device)
+
+    def set_lr(self, lr):
+        """update_scheduler (trainers_ldm_cond.py:783-790): the scheduled lr replaces EVERY
+        group's lr (the per-parameter lr factors of the first step are not re-applied)."""
+        for s in self.seg_hp:
+            s[2] = lr
+        self._upload_segments()
+
+    def _sink(self, p):
+        return self.flat.view_of(p, self.flat.grad), False
+
+    @torch.no_grad()
+    def train_step(self, latents, rgb_latents, loss_mask=None, timesteps=None, noise=None):
+        """One iteration; returns the (local) mean loss as a 0-d fp64 device tensor."""
+        u, sch = self.unet, self.sched
+        B = latents.shape[0]
+        dev = latents.device
+        if noise is None:
+            noise = torch.randn(latents.shape, generator=self.gen, device=dev, dtype=latents.dtype)
+        if timesteps is None:
+            timesteps = torch.randint(self.min_noise_level, sch.num_train_timesteps, (B,), generator=self.gen,
+                                      device=dev, dtype=torch.long)
+        noisy = sch.add_noise(latents, noise, timesteps)
+        sources = [noisy, rgb_latents]
+        if self.self_condition:
+            zeros = torch.zeros_like(noisy)
+            pred0 = u.forward_sources([noisy, rgb_latents, zeros], timesteps)
+            cond = sch.remove_noise(noisy, pred0.float(), timesteps)
+            sources.append(cond)
+        if sch.prediction_type == "epsilon":
+            target = noise
+        elif sch.prediction_type == "sample":
+            target = latents
+        else:
+            raise ValueError(f"Unknown prediction type: {sch.prediction_type}")
+        graph = UNetTrainGraph(u, self._sink, on_ready=self.bucketer.ready)
+        pred = graph.forward(sources, timesteps)              # the conv_in gather casts each source
+        weights = getattr(sch, "weights", None)
+        loss_sum, dpred = K.mse_loss(pred, target, loss_mask, timesteps, weights,
+                                     grad_scale=1.0 / (pred.numel() * self.world))
+        graph.backward(dpred)
+        self.bucketer.finish()
+        self.step_count += 1
+        K.sq_norm(self.flat.grad, out=self.sqsum)
+        K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.segs, len(self.seg_hp),
+                self.step_count, self.betas[0], self.betas[1], self.eps, sqsum=self.sqsum,
+                max_norm=self.clip_grad if self.clip_grad > 0 else 0.0)
+        u.invalidate_packed()
+        return loss_sum / pred.numel()
