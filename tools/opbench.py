@@ -40,10 +40,11 @@ def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, ge
     return run, flops, None
 
 
-def attn_case(B, N, C, heads=8):
+def attn_case(B, N, C, heads=8, legacy=False):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
     def run():
+        K.force_attention_legacy(legacy)
         return K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, C // heads, N, N, 3 * C, 3 * C, 3 * C)
     return run, 4.0 * B * heads * N * N * (C // heads), None
 
@@ -92,6 +93,9 @@ CASES = {
     "conv3_l3_2560": lambda: conv_case(8, 8, 8, 2560, 1280, c1=1280, residual=True, stats=True),
     "conv3_s2_l2": lambda: conv_case(8, 16, 16, 1280, 1280, stride=2, stats=True),
     "attn_4096_d40": lambda: attn_case(8, 4096, 320),
+    "attn_4096_d40_legacy": lambda: attn_case(8, 4096, 320, legacy=True),
+    "attn_1024_d80_legacy": lambda: attn_case(8, 1024, 640, legacy=True),
+    "attn_256_d160_legacy": lambda: attn_case(8, 256, 1280, legacy=True),
     "attn_1024_d80": lambda: attn_case(8, 1024, 640),
     "attn_256_d160": lambda: attn_case(8, 256, 1280),
     "gn_l0_fused": lambda: gn_case(8, 4096, 320, True),

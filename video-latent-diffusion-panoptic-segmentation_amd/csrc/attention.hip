@@ -277,6 +277,260 @@ int launch_t(const AttnArgs& a, int batch, hipStream_t s) {
 
 
 // ======================================================================================
+// bf16 forward on the full-rate v_mfma_f32_16x16x32_bf16 (the 16x16x16 form above issues at
+// half the FLOP rate on gfx950: 16 busy cycles for half the work).
+//   S^T[kv][q]: per 16-key fragment, one x32 MFMA per 32 head-dim columns, the head dim
+//               zero-padded to a multiple of 32 (d = 40 -> 64: a 16x16x16 remainder would cost
+//               the same 16 cycles as the padded x32);  A = K rows (ds_read_b128), B = Q.
+//   O^T[d][q] += V^T P^T over 32 keys per MFMA: the B operand concatenates the bf16-packed S^T
+//               accumulators of key fragments 2t and 2t+1 (k order kv = 32t + 16(j>>2) + 4g +
+//               (j&3)), and the A operand concatenates the two matching ds_read_b64_tr_b16 reads
+//               of V, so the permuted k order is the same on both sides and nothing moves
+//               between lanes.
+// Softmax VALU per score: max3 (half), fma + exp2, half a cvt_pk.
+// ======================================================================================
+// max over the 4 lanes {l, l^16, l^32, l^48} with the gfx950 row-swap permutes (VALU, no LDS
+// round trip as ds_bpermute would take)
+__device__ __forceinline__ float max_over_groups(float v) {
+  unsigned u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  u = __float_as_uint(v);
+  const auto b = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+template <int DP, int QSUB, bool ONES>
+__global__ __launch_bounds__(256, 2) void attn32_kernel(const AttnArgs p) {
+  typedef bf16_t T;
+  constexpr int ES = 2, EPC = 8;
+  constexpr int ND = DP / 16;           // 16-row O^T fragments (P.V covers DP columns)
+  constexpr int DPK = (DP + 31) / 32 * 32;   // Q.K^T head dim, zero-padded to whole x32 chunks
+  constexpr int NC = DPK / 32;
+  constexpr int CPR = DPK / EPC;
+  constexpr int RCH = CPR + 1;
+  constexpr int ROW = RCH * EPC;
+  constexpr int TILE = KVT * ROW;
+  __shared__ uint4 smem[2 * 2 * TILE * ES / 16];
+  T* const lds = reinterpret_cast<T*>(smem);
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 15, g = lane >> 4;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int qbase = blockIdx.x * (64 * QSUB) + wave * 16 * QSUB;
+
+  const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
+  const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
+  const T* vp = reinterpret_cast<const T*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * p.d;
+  const int ones_chunk = ONES ? p.d / EPC : -1;
+
+  auto issue_tile = [&](int kv0, int buf) {
+    const unsigned kb = lds0 + (unsigned)(buf * 2 * TILE * ES);
+    const unsigned vb = kb + TILE * ES;
+    for (int i = wave; i < RCH; i += 4) {
+      const int L = i * 64 + lane;
+      const int row = L / RCH, c = L - row * RCH;
+      const int kv = kv0 + row, d = c * EPC;
+      const bool ok = kv < p.nkv && c < CPR && d < p.d;
+      const void* ks = ok ? (const void*)(kp + (int64_t)kv * p.ks + d) : (const void*)&kZeros16;
+      const void* vs = ok ? (const void*)(vp + (int64_t)kv * p.vs + d)
+                          : (c == ones_chunk ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
+      const unsigned off = __builtin_amdgcn_readfirstlane(i * 64 * 16);
+      glds16(ks, kb + off);
+      glds16(vs, vb + off);
+    }
+  };
+
+  // Q fragments: x32 chunk c: lane holds Q[q][32c + 8g .. +8] (zero past head_dim)
+  Frag8<T> q32[QSUB][NC];
+#pragma unroll
+  for (int s = 0; s < QSUB; ++s) {
+    const int qi = qbase + 16 * s + lr;
+    const T* qrow = qp + (int64_t)qi * p.qs;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int dd = 32 * c + 8 * g;
+      if (qi < p.nq && dd < p.d) q32[s][c].v = *reinterpret_cast<const uint4*>(qrow + dd);
+      else q32[s][c].v = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+
+  f32x4_t oacc[ND][QSUB];
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+#pragma unroll
+    for (int s = 0; s < QSUB; ++s) oacc[i][s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float mrun[QSUB], lrun[QSUB];
+#pragma unroll
+  for (int s = 0; s < QSUB; ++s) { mrun[s] = -INFINITY; lrun[s] = 0.f; }
+  const float c2 = p.scale_log2;
+
+  auto compute = [&](int buf, int kv0, bool masked) {
+    const T* Ks = lds + buf * 2 * TILE;
+    const T* Vs = Ks + TILE;
+    f32x4_t sacc[4][QSUB];
+#pragma unroll
+    for (int js = 0; js < 4; ++js)
+#pragma unroll
+      for (int s = 0; s < QSUB; ++s) sacc[js][s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int js = 0; js < 4; ++js) {
+      const T* krow = Ks + (16 * js + lr) * ROW;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        Frag8<T> ka;
+        ka.v = *reinterpret_cast<const uint4*>(krow + 32 * c + 8 * g);
+#pragma unroll
+        for (int s = 0; s < QSUB; ++s) mma_k32(sacc[js][s], ka, q32[s][c]);
+      }
+    }
+    uint2 pk[4][QSUB];                      // bf16 P^T, (kv 4g .. 4g+3 of fragment js) per lane
+#pragma unroll
+    for (int s = 0; s < QSUB; ++s) {
+      if (masked) {
+#pragma unroll
+        for (int js = 0; js < 4; ++js)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (kv0 + 16 * js + 4 * g + r >= p.nkv) sacc[js][s][r] = -INFINITY;
+      }
+      float m0 = fmaxf(fmaxf(sacc[0][s][0], sacc[0][s][1]), sacc[0][s][2]);
+      float m1 = fmaxf(fmaxf(sacc[0][s][3], sacc[1][s][0]), sacc[1][s][1]);
+      float m2 = fmaxf(fmaxf(sacc[1][s][2], sacc[1][s][3]), sacc[2][s][0]);
+      float m3 = fmaxf(fmaxf(sacc[2][s][1], sacc[2][s][2]), sacc[2][s][3]);
+      float m4 = fmaxf(fmaxf(sacc[3][s][0], sacc[3][s][1]), sacc[3][s][2]);
+      float mx = fmaxf(fmaxf(m0, m1), m2);
+      mx = fmaxf(fmaxf(mx, m3), m4);
+      mx = max_over_groups(fmaxf(mx, sacc[3][s][3]));
+      const float ms = mx * c2;
+      if (__any(ms > mrun[s] + kRescaleThr)) {
+        const float mnew = fmaxf(mrun[s], ms);
+        const float alpha = __builtin_amdgcn_exp2f(mrun[s] - mnew);
+        mrun[s] = mnew;
+        if (!ONES) lrun[s] *= alpha;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) oacc[i][s] *= alpha;
+      }
+      const float mneg = -mrun[s];
+      float lsum = 0.f;
+#pragma unroll
+      for (int js = 0; js < 4; ++js) {
+        float pv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pv[r] = __builtin_amdgcn_exp2f(fmaf(sacc[js][s][r], c2, mneg));
+          if (!ONES) lsum += pv[r];
+        }
+        pk[js][s] = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
+      }
+      if (!ONES) lrun[s] += lsum;
+    }
+    // O^T += V^T P^T, 32 keys per MFMA
+    typedef __attribute__((ext_vector_type(4))) short s4_t;
+    typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+#pragma unroll
+    for (int dd = 0; dd < ND; ++dd) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const T* a0 = Vs + (32 * t + 4 * g + (lr >> 2)) * ROW + 16 * dd + 4 * (lr & 3);
+        const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0)));
+        const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0 + 16 * ROW)));
+        Frag8<T> va;
+        va.v = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+        for (int s = 0; s < QSUB; ++s) {
+          Frag8<T> pb;
+          pb.v = make_uint4(pk[2 * t][s].x, pk[2 * t][s].y, pk[2 * t + 1][s].x, pk[2 * t + 1][s].y);
+          mma_k32(oacc[dd][s], va, pb);
+        }
+      }
+    }
+  };
+
+  const int ntiles = (p.nkv + KVT - 1) / KVT;
+  issue_tile(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) issue_tile((t + 1) * KVT, buf ^ 1);
+    const int kv0 = t * KVT;
+    if (kv0 + KVT > p.nkv) compute(buf, kv0, true);
+    else compute(buf, kv0, false);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  T* op = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * p.d;
+#pragma unroll
+  for (int s = 0; s < QSUB; ++s) {
+    float lt;
+    if constexpr (ONES) {
+      lt = __shfl(oacc[ND - 1][s][0], 32 + lr, 64);
+    } else {
+      lt = lrun[s] + __shfl_xor(lrun[s], 16, 64);
+      lt += __shfl_xor(lt, 32, 64);
+    }
+    const float inv = 1.0f / lt;
+    const int qi = qbase + 16 * s + lr;
+    if (qi >= p.nq) continue;
+    if (p.lse && g == 0) p.lse[((int64_t)b * p.heads + h) * p.nq + qi] = mrun[s] + __log2f(lt);
+#pragma unroll
+    for (int dd = 0; dd < ND; ++dd) {
+      const int d = 16 * dd + 4 * g;
+      if (d >= p.d) continue;
+      *reinterpret_cast<uint2*>(op + (int64_t)qi * p.os + d) =
+          make_uint2(pack_bf16x2(oacc[dd][s][0] * inv, oacc[dd][s][1] * inv),
+                     pack_bf16x2(oacc[dd][s][2] * inv, oacc[dd][s][3] * inv));
+    }
+  }
+}
+
+template <int DP, int QSUB, bool ONES>
+int launch32_cfg(const AttnArgs& a, int batch, hipStream_t s) {
+  dim3 grid((a.nq + 64 * QSUB - 1) / (64 * QSUB), a.heads, batch);
+  hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES>), grid, dim3(256), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+template <int DP>
+int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
+  // query subtiles per wave: as many as stay spill-free (the ONES variant has no l registers)
+  constexpr int QS1 = DP <= 48 ? 4 : (DP <= 96 ? 2 : 1);
+  constexpr int QS0 = DP <= 96 ? 2 : 1;
+  if (a.d == DP - 8) return launch32_cfg<DP, QS1, true>(a, batch, s);
+  return launch32_cfg<DP, QS0, false>(a, batch, s);
+}
+
+int g_attn_legacy = 0;   // tuning / A-B hook: 1 forces the 16x16x16 kernel
+
+// bf16 with 16-byte Q rows: the x32 kernel; otherwise the generic one
+int launch_bf16(const AttnArgs& a, int batch, hipStream_t s) {
+  const int dp = (a.d + 15) / 16 * 16;
+  if (!g_attn_legacy && a.qs % 8 == 0 && a.os % 4 == 0) {
+    switch (dp) {
+      case 48: return launch32_dp<48>(a, batch, s);
+      case 64: return launch32_dp<64>(a, batch, s);
+      case 80: return launch32_dp<80>(a, batch, s);
+      case 96: return launch32_dp<96>(a, batch, s);
+      case 128: return launch32_dp<128>(a, batch, s);
+      case 160: return launch32_dp<160>(a, batch, s);
+      default: break;
+    }
+  }
+  return launch_t<bf16_t>(a, batch, s);
+}
+
+// ======================================================================================
 // Backward (flash-attention-2 style, P recomputed from the saved log2-domain LSE):
 //   D[q]   = sum_d dO[q][d] O[q][d]
 //   P      = 2^(S c2 - lse2[q]),  dP = dO V^T,  dZ = P (dP - D[q])     (Z = scale Q K^T)
@@ -648,8 +902,10 @@ extern "C" int ldm_attention(const ldm_attn_params* q, ldm_stream_t stream) {
   if (st != LDM_OK) return st;
   const AttnArgs a = attn_args(q);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, q->batch, s) : launch_t<float>(a, q->batch, s);
+  return q->dtype == LDM_BF16 ? launch_bf16(a, q->batch, s) : launch_t<float>(a, q->batch, s);
 }
+
+extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
 
 extern "C" int ldm_attention_fwd_lse(const ldm_attn_params* q, float* lse, ldm_stream_t stream) {
   const int st = attn_validate(q);
@@ -658,7 +914,7 @@ extern "C" int ldm_attention_fwd_lse(const ldm_attn_params* q, float* lse, ldm_s
   AttnArgs a = attn_args(q);
   a.lse = lse;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, q->batch, s) : launch_t<float>(a, q->batch, s);
+  return q->dtype == LDM_BF16 ? launch_bf16(a, q->batch, s) : launch_t<float>(a, q->batch, s);
 }
 
 extern "C" size_t ldm_attention_bwd_workspace_bytes(const ldm_attn_params* q) {

@@ -73,6 +73,7 @@ EXPORTS = {
     "ldm_resize_bilinear": (_i, [_vp, _i, _i, _i, _i, _i, _f, _f, _f, _f, _vp, _i, _i, _vp]),
     "ldm_gaussian_posterior": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
     "ldm_attention_fwd_lse": (_i, [ctypes.POINTER(AttnParams), _vp, _vp]),
+    "ldm_attention_force_legacy": (None, [_i]),
     "ldm_attention_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_bwd": (_i, [ctypes.POINTER(AttnParams), _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
     "ldm_group_norm_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
@@ -328,6 +329,11 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
               f"Cin={c0}+{c1} L{out_layout}"
         _prof_stop(ev, "igemm", flops, nbytes, det)
     return out
+
+
+def force_attention_legacy(legacy=True):
+    """Tuning hook: route bf16 attention through the 16x16x16-MFMA kernel (A/B only)."""
+    load_library().ldm_attention_force_legacy(int(bool(legacy)))
 
 
 def force_conv_plan(bm=0, bn=0, ksplit=1):
