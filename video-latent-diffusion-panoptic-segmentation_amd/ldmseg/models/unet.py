@@ -527,7 +527,7 @@ class UNet(nn.Module):
             raise NotImplementedError("class_labels / timestep_cond / attention_mask are not on the reference path")
         if down_block_additional_residuals is not None or mid_block_additional_residual is not None:
             raise NotImplementedError("additional residuals belong to the separate_encoder variant")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
             out = _UNetTrainFn.apply(self, timestep, sample, *self._trainable())
         else:
             out = self.forward_sources([sample], timestep, encoder_hidden_states)
