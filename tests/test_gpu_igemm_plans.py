@@ -30,7 +30,8 @@ def plan():
     K.force_conv_plan(0, 0, 1)
 
 
-PLANS = [(256, 160, 1), (256, 160, 3), (128, 128, 1), (128, 32, 2), (64, 64, 1), (32, 128, 3)]
+PLANS = [(256, 160, 1), (256, 160, 3), (128, 160, 1), (64, 160, 2), (128, 128, 1), (128, 32, 2), (64, 64, 1),
+         (32, 128, 3)]
 SHAPES = [
     # name, B, c0, c1, H, W, Cout, k, stride, upsample
     ("l0", 1, 320, 0, 32, 32, 320, 3, 1, False),
@@ -85,7 +86,8 @@ def test_plan_groupnorm_stats(pl, plan):
     assert rel_err(out.view(B, H, H, -1).permute(0, 3, 1, 2), ref) < 3e-2
 
 
-@pytest.mark.parametrize("pl", [(256, 160, 1), (128, 128, 1), (64, 64, 1)], ids=["256x160", "128x128", "64x64"])
+@pytest.mark.parametrize("pl", [(256, 160, 1), (128, 160, 1), (128, 128, 1), (64, 64, 1)],
+                         ids=["256x160", "128x160", "128x128", "64x64"])
 @pytest.mark.parametrize("M,Kd,N", [(300, 320, 2560), (1024, 640, 640)])
 def test_plan_geglu(M, Kd, N, pl, plan):
     torch.manual_seed(5)

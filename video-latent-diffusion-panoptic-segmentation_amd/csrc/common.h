@@ -34,7 +34,8 @@ template <typename T> __device__ __forceinline__ T from_f(float v);
 template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
 template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return f2bf(v); }
 
-__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + __expf(-x)); }
+// x * sigmoid(x) with v_exp + v_rcp (1 ulp) instead of an IEEE division sequence
+__device__ __forceinline__ float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 // erf via Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 absolute): one v_rcp, one v_exp and a
 // degree-5 Horner chain instead of ocml erff's ~40-instruction path.
 __device__ __forceinline__ float erf_fast(float x) {

@@ -346,6 +346,191 @@ __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0,
   }
 }
 
+// Fast epilogue for the common bf16 cases (NHWC with bias / time embedding / SiLU / residual /
+// GroupNorm partials, and GEGLU): each thread owns 8 consecutive channels (one 16-B store per
+// row), all of a thread's residual and time-embedding loads are issued before any value is
+// finished, and nothing in the row loop branches on the layout.  `stage` is the fp32 tile
+// [ROWS][pitch] in LDS; `red` may alias it (it is written only after a barrier).
+// Returns false (nothing done) when the call needs the generic epilogue_rows.
+__device__ __forceinline__ bool fast_epilogue_ok(const ConvArgs& p) {
+  const auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  return !p.out_f32 && (p.out_layout == LDM_OUT_NHWC || p.out_layout == LDM_OUT_GEGLU) && (p.n & 7) == 0 &&
+         a16(p.out) && a16(p.residual) && a16(p.bias) && a16(p.temb) && (p.temb_stride & 3) == 0;
+}
+__device__ __forceinline__ void unpack8(const uint4 u, float* v) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = __uint_as_float(w[k] << 16);
+    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* v) {
+  bf16_t h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = f2bf(v[k]);
+  return *reinterpret_cast<const uint4*>(h);
+}
+
+// rows [m0, m0 + rows) cover at most two batches (the fast path holds two time embeddings)
+__device__ __forceinline__ bool fast_temb_ok(const ConvArgs& p, int m0, int rows) {
+  return !p.temb || (min(m0 + rows, p.M) - 1) / p.hw_out - m0 / p.hw_out <= 1;
+}
+
+template <int ROWS, int COLS, int NT>
+__device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0, const float* stage, int pitch,
+                                              float* red) {
+  const int tid = threadIdx.x;
+  const int N = p.n;
+  if (p.out_layout == LDM_OUT_GEGLU) {
+    constexpr int OCW = COLS / 16;             // 8-wide output chunks per row
+    constexpr int ORP = NT / OCW;
+    constexpr int ONP = (ROWS + ORP - 1) / ORP;
+    const int oc8 = tid % OCW, r0 = tid / OCW;
+    const int lc = 8 * oc8;
+    const int oc = (n0 >> 1) + lc;
+    if (r0 >= ORP || oc >= (N >> 1)) return;
+    const int pcl = (lc >> 4) * 32 + (lc & 15);
+    const int pc = (oc >> 4) * 32 + (oc & 15);
+    float bh[8], bg[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      bh[k] = p.bias ? p.bias[pc + k] : 0.f;
+      bg[k] = p.bias ? p.bias[pc + 16 + k] : 0.f;
+    }
+    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+#pragma unroll
+    for (int q = 0; q < ONP; ++q) {
+      const int r = r0 + q * ORP;
+      if (r >= ROWS || m0 + r >= p.M) break;
+      const float* srow = stage + r * pitch;
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k += 4) {
+        const float4 h = *reinterpret_cast<const float4*>(srow + pcl + k);
+        const float4 g = *reinterpret_cast<const float4*>(srow + pcl + 16 + k);
+        v[k] = (h.x + bh[k]) * gelu_f(g.x + bg[k]);
+        v[k + 1] = (h.y + bh[k + 1]) * gelu_f(g.y + bg[k + 1]);
+        v[k + 2] = (h.z + bh[k + 2]) * gelu_f(g.z + bg[k + 2]);
+        v[k + 3] = (h.w + bh[k + 3]) * gelu_f(g.w + bg[k + 3]);
+      }
+      *reinterpret_cast<uint4*>(out + (int64_t)(m0 + r) * (N >> 1) + oc) = pack8(v);
+    }
+    return;
+  }
+  constexpr int CW = COLS / 8;                 // 16-B chunks per row
+  constexpr int RP = NT / CW;                  // rows per pass
+  constexpr int NP = (ROWS + RP - 1) / RP;
+  constexpr int HALVES = ROWS >= 64 ? ROWS / 64 : 1;
+  const int c8 = tid % CW, r0 = tid / CW;
+  const int n = n0 + 8 * c8;
+  const bool act = r0 < RP && n < N;
+  const bool stats = p.gn_part != nullptr;
+  float s[HALVES][8], sq[HALVES][8];
+#pragma unroll
+  for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s[hh][k] = 0.f; sq[hh][k] = 0.f; }
+  if (act) {
+    float add[8];
+#pragma unroll
+    for (int k = 0; k < 8; k += 4) {
+      const float4 b4 = p.bias ? *reinterpret_cast<const float4*>(p.bias + n + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      add[k] = b4.x; add[k + 1] = b4.y; add[k + 2] = b4.z; add[k + 3] = b4.w;
+    }
+    const bf16_t* res = reinterpret_cast<const bf16_t*>(p.residual);
+    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+    // the tile's rows span at most two batches (fast_temb_ok): their time embeddings
+    const int b0 = m0 / p.hw_out;
+    const int bsplit = (b0 + 1) * p.hw_out;          // first row of batch b0 + 1
+    float4 te0[2], te1[2];
+    if (p.temb) {
+      const float* tp = p.temb + (int64_t)b0 * p.temb_stride + n;
+      te0[0] = *reinterpret_cast<const float4*>(tp);
+      te0[1] = *reinterpret_cast<const float4*>(tp + 4);
+      if (bsplit < min(m0 + ROWS, p.M)) {
+        te1[0] = *reinterpret_cast<const float4*>(tp + p.temb_stride);
+        te1[1] = *reinterpret_cast<const float4*>(tp + p.temb_stride + 4);
+      } else {
+        te1[0] = te0[0];
+        te1[1] = te0[1];
+      }
+    }
+    constexpr int GP = NP < 3 ? NP : 3;             // rows whose residual loads are in flight together
+#pragma unroll
+    for (int q0 = 0; q0 < NP; q0 += GP) {
+      uint4 rv[GP];
+#pragma unroll
+      for (int q = 0; q < GP; ++q) {
+        const int r = r0 + (q0 + q) * RP;
+        if (res && q0 + q < NP && r < ROWS && m0 + r < p.M)
+          rv[q] = *reinterpret_cast<const uint4*>(res + (int64_t)(m0 + r) * N + n);
+      }
+#pragma unroll
+      for (int q = 0; q < GP; ++q) {
+        const int r = r0 + (q0 + q) * RP;
+        const int m = m0 + r;
+        if (q0 + q >= NP || r >= ROWS || m >= p.M) break;
+        const float* srow = stage + r * pitch + 8 * c8;
+        const float4 x0 = *reinterpret_cast<const float4*>(srow);
+        const float4 x1 = *reinterpret_cast<const float4*>(srow + 4);
+        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += add[k];
+        if (p.temb) {
+          const bool second = m >= bsplit;
+          const float4 ta = second ? te1[0] : te0[0], tb = second ? te1[1] : te0[1];
+          v[0] += ta.x; v[1] += ta.y; v[2] += ta.z; v[3] += ta.w;
+          v[4] += tb.x; v[5] += tb.y; v[6] += tb.z; v[7] += tb.w;
+        }
+        if (p.act == LDM_ACT_SILU) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = silu_f(v[k]);
+        }
+        if (res) {
+          float rr[8];
+          unpack8(rv[q], rr);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] += rr[k];
+        }
+        const uint4 packed = pack8(v);
+        *reinterpret_cast<uint4*>(out + (int64_t)m * N + n) = packed;
+        if (stats) {
+          float st[8];
+          unpack8(packed, st);                   // statistics of the value as stored
+          const int hh = HALVES > 1 ? (r >> 6) : 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { s[hh][k] += st[k]; sq[hh][k] += st[k] * st[k]; }
+        }
+      }
+    }
+  }
+  if (!stats) return;
+  __syncthreads();                             // every stage read is done: red may alias it
+  if (r0 < RP) {
+#pragma unroll
+    for (int hh = 0; hh < HALVES; ++hh)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        red[((r0 * CW + c8) * HALVES + hh) * 16 + 2 * k] = s[hh][k];
+        red[((r0 * CW + c8) * HALVES + hh) * 16 + 2 * k + 1] = sq[hh][k];
+      }
+  }
+  __syncthreads();
+  for (int e = tid; e < CW * HALVES * 8; e += NT) {
+    const int k = e & 7, hh = (e >> 3) % HALVES, c = e / (8 * HALVES);
+    const int nn = n0 + 8 * c + k;
+    const int chunk = (m0 >> 6) + hh;
+    if (nn >= N || chunk * 64 >= p.M) continue;
+    float a = 0.f, b = 0.f;
+    for (int rg = 0; rg < RP; ++rg) {
+      a += red[((rg * CW + c) * HALVES + hh) * 16 + 2 * k];
+      b += red[((rg * CW + c) * HALVES + hh) * 16 + 2 * k + 1];
+    }
+    p.gn_part[(int64_t)chunk * N + nn] = make_float2(a, b);
+  }
+}
+
 template <typename T, int BM, int BN, bool DMA>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   constexpr int ES = sizeof(T);
@@ -357,7 +542,11 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   constexpr int FN = BN / 32;
   constexpr int SMEM_MAIN = 2 * (BM + BN) * 8;           // uint4
   constexpr int PITCH = BN + 4;                          // staged fp32 row pitch
-  constexpr int SMEM_EPI = (BM * PITCH + 3) / 4;         // uint4
+  // the fp32 tile is staged in two row halves when a whole one would not fit the ring (128x160:
+  // keeps the block at 73.7 KB of LDS so two blocks share a CU)
+  constexpr int EPI_H = (BM * PITCH * 4 > SMEM_MAIN * 16 && BM >= 128) ? 2 : 1;
+  constexpr int EPI_ROWS = BM / EPI_H;
+  constexpr int SMEM_EPI = (EPI_ROWS * PITCH + 3) / 4;   // uint4
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   __shared__ uint4 smem[SMEM];
 
@@ -589,26 +778,44 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   }
 
   // ------------------------------------------------------------------ fused epilogue
-  // phase 1: raw accumulators -> LDS [BM][PITCH] fp32
+  // phase 1: raw accumulators -> LDS [EPI_ROWS][PITCH] fp32 (per row half when EPI_H == 2:
+  // wave row wm owns rows [wm * BM/2, (wm+1) * BM/2) = half wm)
   float* stage = reinterpret_cast<float*>(smem);
-#pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int ml = wm * (BM / 2) + i * 16 + lr;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int nl = wn * (BN / 2) + j * 16 + 4 * g;
-      *reinterpret_cast<float4*>(stage + ml * PITCH + nl) =
-          make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-    }
-  }
-  __syncthreads();
-  // phase 2: coalesced rows; the statistics reduction reuses the space past the stage
   float* red = stage;  // overwritten only after every thread has read its stage values
   auto raw = [&](int r, int c4, float* v) {
     const float4 x = *reinterpret_cast<const float4*>(stage + r * PITCH + 4 * c4);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
   };
-  epilogue_rows<T, BM, BN, 256>(p, m0, n0, raw, red);
+  bool fast = false;
+  if constexpr (sizeof(T) == 2 && EPI_ROWS >= 64) fast = fast_epilogue_ok(p);
+#pragma unroll
+  for (int h = 0; h < EPI_H; ++h) {
+    if (h > 0) __syncthreads();   // the previous half (and its reduction scratch) is consumed
+    if (EPI_H == 1 || wm == h) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ml = (EPI_H == 1 ? wm * (BM / 2) : 0) + i * 16 + lr;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int nl = wn * (BN / 2) + j * 16 + 4 * g;
+          *reinterpret_cast<float4*>(stage + ml * PITCH + nl) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+      }
+    }
+    __syncthreads();
+    // phase 2: coalesced rows
+    const int mh = m0 + h * EPI_ROWS;
+    if (mh < p.M) {
+      if constexpr (sizeof(T) == 2 && EPI_ROWS >= 64) {
+        if (fast && fast_temb_ok(p, mh, EPI_ROWS)) {
+          epilogue_fast<EPI_ROWS, BN, 256>(p, mh, n0, stage, PITCH, red);
+          continue;
+        }
+      }
+      epilogue_rows<T, EPI_ROWS, BN, 256>(p, mh, n0, raw, red);
+    }
+  }
 }
 
 // Split-K reduction + full epilogue: one block per 64-row x 128-channel tile.
@@ -651,11 +858,11 @@ constexpr int STAGE_U4 = (BM + BN) * 8;          // uint4 per ring stage (53,248
 constexpr int NSTAGE = 3;
 constexpr int EPI_ROWS = 128;                      // epilogue staged in two row halves
 constexpr int PITCH = BN + 4;
-constexpr int RED_FLOATS = (NT / (BN / 4)) * (BN / 4) * (EPI_ROWS / 64) * 4 * 2;
+constexpr int RED_FLOATS = (NT / (BN / 8)) * (BN / 8) * (EPI_ROWS / 64) * 16;   // epilogue_fast layout (>= epilogue_rows')
 static_assert(EPI_ROWS * PITCH + RED_FLOATS <= NSTAGE * STAGE_U4 * 4, "epilogue does not fit the ring");
 }  // namespace big
 
-template <int MODE>   // experiment: 0 normal, 1 no operand loads, 2 no MFMA
+template <int MODE>   // experiment: 0 normal, 1 no operand loads, 2 no MFMA, 3 no epilogue, 4 MFMA only
 __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
   using namespace big;
   typedef bf16_t T;
@@ -786,8 +993,8 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
   };
 
   // ---- 3-stage ring: prologue fills stages 0 and 1
-  if (MODE != 1 && kt0 < kt1) issue(kt0, 0);
-  if (MODE != 1 && kt0 + 1 < kt1) issue(kt0 + 1, 1);
+  if (MODE != 1 && MODE != 4 && kt0 < kt1) issue(kt0, 0);
+  if (MODE != 1 && MODE != 4 && kt0 + 1 < kt1) issue(kt0 + 1, 1);
   int st = 0;
   for (int kt = kt0; kt < kt1; ++kt) {
     if (kt + 1 < kt1) {           // leave tile kt+1's instructions in flight
@@ -798,7 +1005,7 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
     }
     // every wave's tile kt has landed, and every wave is done reading stage (kt-1) % 3
     asm volatile("s_barrier" ::: "memory");
-    if (MODE != 1 && kt + 2 < kt1) issue(kt + 2, st == 0 ? 2 : st - 1);
+    if (MODE != 1 && MODE != 4 && kt + 2 < kt1) issue(kt + 2, st == 0 ? 2 : st - 1);
     if (MODE != 2) compute(st);
     st = st == 2 ? 0 : st + 1;
   }
@@ -824,9 +1031,19 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
     return;
   }
 
+  if (MODE >= 3) {   // ablation: keep the accumulators alive, skip the epilogue
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 12345.f) reinterpret_cast<float*>(p.out)[tid] = t;
+    return;
+  }
   // ---- fused epilogue, two halves of 128 rows (waves wm = 2h, 2h+1 own half h)
   float* stage = reinterpret_cast<float*>(smem);
   float* red = stage + EPI_ROWS * PITCH;
+  const bool fast = fast_epilogue_ok(p);
   auto raw = [&](int r, int c4, float* v) {
     const float4 x = *reinterpret_cast<const float4*>(stage + r * PITCH + 4 * c4);
     v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
@@ -847,7 +1064,11 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
       }
     }
     __syncthreads();
-    if (m0 + h * EPI_ROWS < p.M) epilogue_rows<T, EPI_ROWS, BN, NT>(p, m0 + h * EPI_ROWS, n0, raw, red);
+    if (m0 + h * EPI_ROWS < p.M) {
+      if (fast && fast_temb_ok(p, m0 + h * EPI_ROWS, EPI_ROWS))
+        epilogue_fast<EPI_ROWS, BN, NT>(p, m0 + h * EPI_ROWS, n0, stage, PITCH, red);
+      else epilogue_rows<T, EPI_ROWS, BN, NT>(p, m0 + h * EPI_ROWS, n0, raw, red);
+    }
   }
 }
 
@@ -871,6 +1092,9 @@ int launch_bm_bn(ConvArgs a, hipStream_t s) {
 
 template <typename T, int BM>
 int launch_bm(const ConvArgs& a, hipStream_t s, int bn) {
+  if constexpr (sizeof(T) == 2 && BM >= 64) {
+    if (bn == 160) return launch_bm_bn<T, BM, 160>(a, s);
+  }
   if (bn == 32) return launch_bm_bn<T, BM, 32>(a, s);
   if (bn == 64) return launch_bm_bn<T, BM, 64>(a, s);
   return launch_bm_bn<T, BM, 128>(a, s);
@@ -888,7 +1112,9 @@ int launch_big(ConvArgs a, hipStream_t s) {
   a.tiles_n = (a.n + big::BN - 1) / big::BN;
   const int tiles_m = (a.M + big::BM - 1) / big::BM;
   a.nblk = tiles_m * a.tiles_n * a.ksplit;
-  if (g_big_mode == 1) hipLaunchKernelGGL(igemm_big_kernel<1>, dim3(a.nblk), dim3(big::NT), 0, s, a);
+  if (g_big_mode == 3) hipLaunchKernelGGL(igemm_big_kernel<3>, dim3(a.nblk), dim3(big::NT), 0, s, a);
+  else if (g_big_mode == 4) hipLaunchKernelGGL(igemm_big_kernel<4>, dim3(a.nblk), dim3(big::NT), 0, s, a);
+  else if (g_big_mode == 1) hipLaunchKernelGGL(igemm_big_kernel<1>, dim3(a.nblk), dim3(big::NT), 0, s, a);
   else if (g_big_mode == 2) hipLaunchKernelGGL(igemm_big_kernel<2>, dim3(a.nblk), dim3(big::NT), 0, s, a);
   else hipLaunchKernelGGL(igemm_big_kernel<0>, dim3(a.nblk), dim3(big::NT), 0, s, a);
   LDM_CHECK_LAUNCH();
@@ -943,6 +1169,15 @@ Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
     pl.bm = M <= 32 ? 32 : (M <= 64 ? 64 : 128);
     pl.bn = 128;
     if (tiles_of(pl.bm, 128) < 256) pl.bn = 64;
+    return pl;
+  }
+  // 128x160 / 64x160 (two blocks per CU, one block's epilogue under the other's MFMAs) beat the
+  // one-block-per-CU 256x160 kernel wherever they still give >= 512 / 400 tiles (opbench sweeps
+  // at the UNet shapes, profiles/r01c_*)
+  const int t128 = tiles_of(128, 160), t64 = tiles_of(64, 160);
+  if (es == 2 && waste_ok && t128 >= 512) { pl.bm = 128; pl.bn = 160; return pl; }
+  if (es == 2 && waste_ok && t64 >= 400 && nk <= 128 && (tiles_big < 240 || nk < 40)) {
+    pl.bm = 64; pl.bn = 160;
     return pl;
   }
   if (big_ok && waste_ok && nk >= 40) {
@@ -1023,7 +1258,8 @@ bool is_mixed(const ldm_conv_params* q, int es) {
 extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
   g_big_mode = bm > 256 ? bm - 256 : 0;
   if (bm > 256) bm = 256;
-  const bool ok = (bm == 256) || ((bm == 32 || bm == 64 || bm == 128) && (bn == 32 || bn == 64 || bn == 128));
+  const bool ok = (bm == 256) || ((bm == 32 || bm == 64 || bm == 128) && (bn == 32 || bn == 64 || bn == 128)) ||
+                  ((bm == 64 || bm == 128) && bn == 160);
   g_force_bm = ok ? bm : 0;
   g_force_bn = ok ? bn : 0;
   g_force_ks = ok ? std::max(1, ksplit) : 0;

@@ -54,34 +54,48 @@ __global__ __launch_bounds__(256) void gn_partial(const T* __restrict__ x, int C
   }
 }
 
-// one wave per (batch, group): fp64 sum of the partials, then the group's scale/shift entries
+// one 256-thread block per (batch, group): fp64 sum of the partials (each thread's loads are
+// unrolled 4-wide so they are in flight together — the partials are L2-resident, so this is a
+// latency problem, not a bandwidth one), then the group's scale/shift entries
 __global__ __launch_bounds__(256) void gn_finalize(const float2* __restrict__ part0, const float2* __restrict__ part1,
                                                    int c0, int c1, int hw, int chunks, int groups, float eps,
                                                    const float* __restrict__ gamma, const float* __restrict__ beta,
                                                    float2* __restrict__ table, float2* __restrict__ save) {
   const int b = blockIdx.x;
-  const int gi = blockIdx.y * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (gi >= groups) return;
+  const int gi = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int C = c0 + c1, cpg = C / groups;
   const int n = chunks * cpg;
   double a = 0.0, q = 0.0;
-  for (int i = lane; i < n; i += 64) {
-    const int ch = i / cpg, c = gi * cpg + (i - ch * cpg);
-    const int64_t row = (int64_t)b * chunks + ch;
-    const float2 v = c < c0 ? part0[row * c0 + c] : part1[row * c1 + (c - c0)];
-    a += v.x;
-    q += v.y;
+  for (int i0 = tid; i0 < n; i0 += 4 * 256) {
+    float2 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 256;
+      v[u] = make_float2(0.f, 0.f);
+      if (i < n) {
+        const int ch = i / cpg, c = gi * cpg + (i - ch * cpg);
+        const int64_t row = (int64_t)b * chunks + ch;
+        v[u] = c < c0 ? part0[row * c0 + c] : part1[row * c1 + (c - c0)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { a += v[u].x; q += v[u].y; }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); q += __shfl_xor(q, o, 64); }
+  __shared__ double red[4][2];
+  if (lane == 0) { red[wave][0] = a; red[wave][1] = q; }
+  __syncthreads();
+  a = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+  q = red[0][1] + red[1][1] + red[2][1] + red[3][1];
   const double cnt = (double)hw * cpg;
   const double mean = a / cnt;
   double var = q / cnt - mean * mean;
   if (var < 0.0) var = 0.0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  if (save && lane == 0) save[(int64_t)b * groups + gi] = make_float2((float)mean, rstd);   // for the backward
-  for (int k = lane; k < cpg; k += 64) {
+  if (save && tid == 0) save[(int64_t)b * groups + gi] = make_float2((float)mean, rstd);   // for the backward
+  for (int k = tid; k < cpg; k += 256) {
     const int c = gi * cpg + k;
     const float sc = rstd * gamma[c];
     table[(int64_t)b * C + c] = make_float2(sc, beta[c] - (float)mean * sc);
@@ -268,7 +282,7 @@ int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw,
     LDM_CHECK_LAUNCH();
     part1 = dst;
   }
-  hipLaunchKernelGGL(gn_finalize, dim3(batch, (groups + 3) / 4), dim3(256), 0, s, part0, part1, c0, c1, hw, chunks,
+  hipLaunchKernelGGL(gn_finalize, dim3(batch, groups), dim3(256), 0, s, part0, part1, c0, c1, hw, chunks,
                      groups, eps, gamma, beta, table, reinterpret_cast<float2*>(save));
   LDM_CHECK_LAUNCH();
   const int64_t nvec = (int64_t)batch * hw * (C / EPC);
