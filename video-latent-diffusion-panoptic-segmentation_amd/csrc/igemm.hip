@@ -531,6 +531,30 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
   }
 }
 
+// Split-K: raw fp32 accumulators of a staged [ROWS][pitch] tile -> this split's slab
+// [M][N] as full coalesced rows (16 B per lane; a 160-column row is 640 contiguous bytes).
+template <int ROWS, int COLS, int NT>
+__device__ __forceinline__ void write_partial_rows(const ConvArgs& p, float* part, int m0, int n0,
+                                                   const float* stage, int pitch) {
+  constexpr int CW = COLS / 4, RP = NT / CW, NP = (ROWS + RP - 1) / RP;
+  const int tid = threadIdx.x, c4 = tid % CW, r0 = tid / CW;
+  const int n = n0 + 4 * c4;
+  if (r0 >= RP || n >= p.n) return;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const int r = r0 + q * RP, m = m0 + r;
+    if (r >= ROWS || m >= p.M) break;
+    const float4 x = *reinterpret_cast<const float4*>(stage + r * pitch + 4 * c4);
+    float* dst = part + (int64_t)m * p.n + n;
+    if (n + 3 < p.n) {
+      *reinterpret_cast<float4*>(dst) = x;
+    } else {
+      const float v[4] = {x.x, x.y, x.z, x.w};
+      for (int k = 0; k < 4 && n + k < p.n; ++k) dst[k] = v[k];
+    }
+  }
+}
+
 template <typename T, int BM, int BN, bool DMA>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   constexpr int ES = sizeof(T);
@@ -755,28 +779,6 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     }
   }
 
-  // ------------------------------------------------------------------ split-K: raw partials
-  if (p.ksplit > 1) {
-    float* part = p.partial + (int64_t)split * p.M * p.n;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * (BM / 2) + i * 16 + lr;
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wn * (BN / 2) + j * 16 + 4 * g;
-        if (n >= p.n) continue;
-        float* dst = part + (int64_t)m * p.n + n;
-        if (n + 3 < p.n) {
-          *reinterpret_cast<float4*>(dst) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-        } else {
-          for (int r = 0; r < 4 && n + r < p.n; ++r) dst[r] = acc[i][j][r];
-        }
-      }
-    }
-    return;
-  }
-
   // ------------------------------------------------------------------ fused epilogue
   // phase 1: raw accumulators -> LDS [EPI_ROWS][PITCH] fp32 (per row half when EPI_H == 2:
   // wave row wm owns rows [wm * BM/2, (wm+1) * BM/2) = half wm)
@@ -806,6 +808,10 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     __syncthreads();
     // phase 2: coalesced rows
     const int mh = m0 + h * EPI_ROWS;
+    if (p.ksplit > 1) {
+      write_partial_rows<EPI_ROWS, BN, 256>(p, p.partial + (int64_t)split * p.M * p.n, mh, n0, stage, PITCH);
+      continue;
+    }
     if (mh < p.M) {
       if constexpr (sizeof(T) == 2 && EPI_ROWS >= 64) {
         if (fast && fast_temb_ok(p, mh, EPI_ROWS)) {
@@ -821,26 +827,59 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
 // Split-K reduction + full epilogue: one block per 64-row x 128-channel tile.
 template <typename T>
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) {
-  __shared__ float red[(256 / 32) * 32 * 1 * 4 * 2];
+  constexpr int ROWS = 64, COLS = 128, PITCH = COLS + 4, RPQ = 256 / (COLS / 4);   // 8 rows per pass
+  __shared__ float stage[ROWS * PITCH];   // also the statistics scratch of either epilogue
   const int tiles_n = (p.n + 127) / 128;
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
   const int m0 = tm * 64, n0 = tn * 128;
   const int64_t slab = (int64_t)p.M * p.n;
-  auto raw = [&](int r, int c4, float* v) {
-    const int m = m0 + r, n = n0 + 4 * c4;
-    const float* src = p.partial + (int64_t)m * p.n + n;
-    v[0] = v[1] = v[2] = v[3] = 0.f;
-    if (n + 3 < p.n) {
-      for (int s = 0; s < p.ksplit; ++s) {
-        const float4 x = *reinterpret_cast<const float4*>(src + s * slab);
-        v[0] += x.x; v[1] += x.y; v[2] += x.z; v[3] += x.w;
+  // phase A: sum the slabs into LDS; per split, the 8 rows of a thread are loaded together
+  {
+    const int c4 = threadIdx.x % (COLS / 4), r0 = threadIdx.x / (COLS / 4);
+    const int n = n0 + 4 * c4;
+    const bool vec = n + 3 < p.n;
+    float4 acc[ROWS / RPQ];
+#pragma unroll
+    for (int q = 0; q < ROWS / RPQ; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int sp = 0; sp < p.ksplit; ++sp) {
+      const float* src = p.partial + sp * slab;
+      float4 x[ROWS / RPQ];
+#pragma unroll
+      for (int q = 0; q < ROWS / RPQ; ++q) {
+        const int m = m0 + r0 + q * RPQ;
+        x[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m < p.M && n < p.n) {
+          const float* e = src + (int64_t)m * p.n + n;
+          if (vec) {
+            x[q] = *reinterpret_cast<const float4*>(e);
+          } else {
+            x[q].x = e[0];
+            if (n + 1 < p.n) x[q].y = e[1];
+            if (n + 2 < p.n) x[q].z = e[2];
+          }
+        }
       }
-    } else {
-      for (int s = 0; s < p.ksplit; ++s)
-        for (int r2 = 0; r2 < 4 && n + r2 < p.n; ++r2) v[r2] += src[s * slab + r2];
+#pragma unroll
+      for (int q = 0; q < ROWS / RPQ; ++q) {
+        acc[q].x += x[q].x; acc[q].y += x[q].y; acc[q].z += x[q].z; acc[q].w += x[q].w;
+      }
     }
+#pragma unroll
+    for (int q = 0; q < ROWS / RPQ; ++q)
+      *reinterpret_cast<float4*>(stage + (r0 + q * RPQ) * PITCH + 4 * c4) = acc[q];
+  }
+  __syncthreads();
+  if constexpr (sizeof(T) == 2) {
+    if (fast_epilogue_ok(p) && fast_temb_ok(p, m0, ROWS)) {
+      epilogue_fast<ROWS, COLS, 256>(p, m0, n0, stage, PITCH, stage);
+      return;
+    }
+  }
+  auto raw = [&](int r, int c4, float* v) {
+    const float4 x = *reinterpret_cast<const float4*>(stage + r * PITCH + 4 * c4);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
   };
-  epilogue_rows<T, 64, 128, 256>(p, m0, n0, raw, red);
+  epilogue_rows<T, ROWS, COLS, 256>(p, m0, n0, raw, stage);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1010,27 +1049,6 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
     st = st == 2 ? 0 : st + 1;
   }
 
-  if (p.ksplit > 1) {
-    float* part = p.partial + (int64_t)split * p.M * p.n;
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int m = m0 + wm * 64 + i * 16 + lr;
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int n = n0 + wn * 80 + j * 16 + 4 * g;
-        if (n >= p.n) continue;
-        float* dst = part + (int64_t)m * p.n + n;
-        if (n + 3 < p.n) {
-          *reinterpret_cast<float4*>(dst) = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-        } else {
-          for (int r = 0; r < 4 && n + r < p.n; ++r) dst[r] = acc[i][j][r];
-        }
-      }
-    }
-    return;
-  }
-
   if (MODE >= 3) {   // ablation: keep the accumulators alive, skip the epilogue
     float t = 0.f;
 #pragma unroll
@@ -1064,6 +1082,11 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
       }
     }
     __syncthreads();
+    if (p.ksplit > 1) {
+      write_partial_rows<EPI_ROWS, BN, NT>(p, p.partial + (int64_t)split * p.M * p.n, m0 + h * EPI_ROWS, n0, stage,
+                                           PITCH);
+      continue;
+    }
     if (m0 + h * EPI_ROWS < p.M) {
       if (fast && fast_temb_ok(p, m0 + h * EPI_ROWS, EPI_ROWS))
         epilogue_fast<EPI_ROWS, BN, NT>(p, m0 + h * EPI_ROWS, n0, stage, PITCH, red);
@@ -1180,9 +1203,16 @@ Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
     pl.bm = 64; pl.bn = 160;
     return pl;
   }
+  // deep K over fewer tiles: 128x160 split to ~512 blocks (<= 8 ways; the coalesced fp32 slab
+  // stays small enough at the 16x16 / 8x8 levels)
+  if (es == 2 && waste_ok && split_ok && nk >= 64) {
+    pl.bm = 128; pl.bn = 160;
+    pl.ksplit = std::max(1, std::min(std::min(8, nk / 16), (512 + t128 / 2) / t128));
+    return pl;
+  }
   if (big_ok && waste_ok && nk >= 40) {
     if (tiles_big >= 240) { pl.bm = 256; pl.bn = 160; return pl; }
-    if (tiles_big >= 96 && nk >= 64 && split_ok) {
+    if (split_ok && ((tiles_big >= 96 && nk >= 64) || (tiles_big >= 48 && nk >= 128))) {
       pl.bm = 256; pl.bn = 160;
       pl.ksplit = std::min((256 + tiles_big - 1) / tiles_big, std::min(4, nk / 32));
       return pl;
