@@ -204,6 +204,27 @@ int ldm_bit_decode(const void* planes, int batch, int n, int64_t hw, int drop_31
                    int dtype, ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Panoptic head (config 4 post-processing).
+ * Replaces: the per-image CPU loop of TrainerDiffusion.compute_pq
+ * (ldmseg/trainers/trainers_ldm_cond.py:1287-1330) and the argmax / confidence threshold of
+ * decode_latents (:426-435).  logits: NCHW fp32 [batch][k][hw].
+ * ldm_panoptic_pixels: pred[b][p] = argmax_k (first maximal index), set to ignore_label where
+ *   the confidence (conf_mode 1: max softmax prob, 2: top1 - top2 prob; 0: no threshold)
+ *   is < mask_th; counts[b][k] = #(pred == k); mask_counts[b][k] = #(sigmoid(logit_k) >= mask_th).
+ *   counts / mask_counts are zeroed here (async memset on `stream`).
+ * ldm_panoptic_finalize: keep[b][k] = k != ignore_label && counts >= count_th &&
+ *   !(counts / mask_counts < overlap_th) (float64; a zero mask count keeps the label, as
+ *   numpy's inf does); out[b][p] = keep[pred] ? pred + 1 : 0  (the reference's cleaned_pred + 1).
+ * k <= 1024.
+ * ------------------------------------------------------------------------------------- */
+int ldm_panoptic_pixels(const float* logits, int batch, int k, int hw, int conf_mode, float mask_th,
+                        int ignore_label, int32_t* pred, int32_t* counts, int32_t* mask_counts,
+                        ldm_stream_t stream);
+int ldm_panoptic_finalize(const int32_t* pred, const int32_t* counts, const int32_t* mask_counts,
+                          int batch, int k, int hw, int count_th, double overlap_th, int ignore_label,
+                          int32_t* keep, int32_t* out, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * Layout / resampling helpers on the path boundary.
  * ldm_nchw_to_nhwc: gathers up to 3 NCHW sources (the sampler's [x_t || rgb || cond] concat,
  * trainers_ldm_cond.py:1134-1141) into one NHWC tensor with c_pad channels (zero filled).

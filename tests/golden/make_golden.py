@@ -11,6 +11,10 @@ What is pinned (each array is data: inputs + the reference's outputs):
   ddim.npz   DDIMNoiseScheduler       ldmseg/schedulers/ddim_scheduler.py:32-269
   vae.npz    GeneralVAESeg            ldmseg/models/vae.py:42-323 (gaussian, no mid blocks)
   vpq.npz    eval_dvpq.vpq_eval       eval/eval_dvpq.py:25-101
+  panoptic.npz  TrainerDiffusion.compute_pq's per-image panoptic head
+             ldmseg/trainers/trainers_ldm_cond.py:1185-1330, run as the reference method on a
+             stand-in trainer whose sample/decode_latents return seeded logits; the
+             cleaned_pred each image hands to CityscapesPanopticEvaluator.add_image is recorded
 
 The UNet has no golden vector: its arithmetic lives in the un-vendored `diffusers`
 package — parity for it is pinned per op against torch.nn.functional.
@@ -281,9 +285,103 @@ def gen_vpq():
     print("vpq.npz:", len(out), "arrays")
 
 
+# --------------------------------------------------------------------------------------
+# panoptic head: the reference compute_pq method itself, on a stand-in trainer
+# --------------------------------------------------------------------------------------
+class _HostTensor(torch.Tensor):
+    """`.cuda()` stays on the host (the fixture container has no GPU)."""
+
+    def cuda(self, *a, **k):
+        return self.as_subclass(torch.Tensor)
+
+
+class _Loader:
+    def __init__(self, batches):
+        self.batches = batches
+        self.dataset = types.SimpleNamespace(meta_data={})
+
+    def __iter__(self):
+        return iter(self.batches)
+
+    def __len__(self):
+        return len(self.batches)
+
+
+def _smooth_logits(gen, B, K, H, W, cell=12):
+    """Segmentation-like logits: a blobby label map whose class gets a spatially varying boost
+    over a negative background, a second class partly competing, and per-pixel noise — so the
+    fixture exercises kept segments, the confidence threshold, small-count and low-overlap drops."""
+    up = lambda t: torch.nn.functional.interpolate(t, size=(H, W), mode="bilinear", align_corners=False)
+    field = up(torch.randn(B, K, max(2, H // cell), max(2, W // cell), generator=gen))
+    lab = field.argmax(1)                                           # blobby label map
+    second = field.topk(2, dim=1).indices[:, 1]
+    boost = 1.0 + 6.0 * up(torch.rand(B, 1, max(2, H // 16), max(2, W // 16), generator=gen))[:, 0]
+    x = torch.randn(B, K, H, W, generator=gen) - 4.0
+    x.scatter_add_(1, lab[:, None], boost[:, None])
+    x.scatter_add_(1, second[:, None], (0.6 * boost)[:, None] * (torch.rand(B, 1, H, W, generator=gen) < 0.5))
+    # fp16-representable values, so the fixture stores them exactly as fp16
+    return x.half().float()
+
+
+def gen_panoptic():
+    import ldmseg.evaluations.cityscapes_pap_eval as cpe
+    from ldmseg.trainers.trainers_ldm_cond import TrainerDiffusion
+
+    recorded = []
+    cpe.CityscapesPanopticEvaluator.add_image = lambda self, pred, gt: recorded.append(np.array(pred))
+    cpe.CityscapesPanopticEvaluator.evaluate = lambda self: {"pq": 0.0, "sq": 0.0, "rq": 0.0}
+    gen = torch.Generator().manual_seed(77)
+    cases = [
+        # name, B, K, H, W, mask_th, count_th, overlap_th, ignore_label, threshold_output, mode, (Hi, Wi), (h, w)
+        ("kitti_max", 2, 30, 48, 64, 0.5, 100, 0.5, 255, True, "max", None, None),
+        ("kitti_ign0", 2, 30, 48, 64, 0.5, 60, 0.5, 0, True, "max", None, None),
+        ("topk_diff", 1, 19, 40, 56, 0.3, 50, 0.7, 255, True, "topk_diff", None, None),
+        ("no_threshold", 1, 16, 32, 32, 0.5, 0, 0.5, 255, False, "max", None, None),
+        ("base_yaml", 1, 48, 80, 112, 0.5, 512, 0.5, 255, True, "max", None, None),
+        ("resized", 1, 20, 32, 48, 0.5, 80, 0.5, 255, True, "max", (64, 96), (80, 120)),
+    ]
+    out = {}
+    for (name, B, K, H, W, mth, cth, oth, ign, thr, mode, img_hw, orig_hw) in cases:
+        logits = _smooth_logits(gen, B, K, H, W, cell=24 if cth >= 512 else 12)
+        Hi, Wi = img_hw or (H, W)
+        h, w = orig_hw or (Hi, Wi)
+        pad = torch.zeros(B, Hi, Wi, dtype=torch.bool)
+        pad[:, : Hi - (Hi // 8 if img_hw else 0), :] = True            # padded bottom rows when resized
+        batch = {
+            "meta": [{"image_file": f"f{i}", "image_id": i, "im_size": (h, w)} for i in range(B)],
+            "image": torch.zeros(B, 3, Hi, Wi),
+            "mask": pad.as_subclass(_HostTensor),
+            "text": [""] * B,
+            "semseg": torch.zeros(B, h, w, dtype=torch.int64).as_subclass(_HostTensor),
+        }
+        sched = types.SimpleNamespace(set_timesteps_inference=lambda num_inference_steps: None,
+                                      move_timesteps_to=lambda dev: None, timesteps=torch.tensor([19]))
+        fake = types.SimpleNamespace(
+            noise_scheduler=sched, args={"gpu": "cpu"}, dl_val=None, rgb_size=64,
+            vae_image=types.SimpleNamespace(encode=None, scaling_factor=1.0),
+            ds=types.SimpleNamespace(ignore_label=ign), mask_th=mth, count_th=cth, overlap_th=oth,
+            encode_inputs=lambda *a, **k: (torch.zeros(B, 4, 8, 8), None),
+            sample=lambda *a, **k: torch.zeros(B, 4, 8, 8),
+            decode_latents=lambda *a, **k: logits.clone(),
+        )
+        fake.crop_padding = types.MethodType(TrainerDiffusion.crop_padding, fake)
+        recorded.clear()
+        TrainerDiffusion.compute_pq(fake, num_inference_steps=1, threshold_output=thr, dataloader=_Loader([batch]),
+                                    threshold_mode=mode)
+        assert len(recorded) == B
+        out[f"{name}__logits"] = logits.half().numpy()
+        out[f"{name}__cleaned"] = np.stack(recorded).astype(np.int16)
+        out[f"{name}__cfg"] = np.array([mth, cth, oth, ign, int(thr), {"max": 1, "topk_diff": 2}[mode],
+                                        Hi, Wi, h, w, Hi - (Hi // 8 if img_hw else 0)], np.float64)
+    out["names"] = np.array([c[0] for c in cases])
+    np.savez_compressed(os.path.join(HERE, "panoptic.npz"), **out)
+    print("panoptic.npz:", len(out), "arrays")
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     gen_codec()
     gen_ddim()
     gen_vae()
     gen_vpq()
+    gen_panoptic()

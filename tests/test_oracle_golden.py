@@ -95,3 +95,26 @@ def test_vpq_eval():
         np.testing.assert_array_equal(tp, z[f"c{c}__tp"])
         np.testing.assert_array_equal(fn, z[f"c{c}__fn"])
         np.testing.assert_array_equal(fp, z[f"c{c}__fp"])
+
+
+def _panoptic_cases():
+    z = load("panoptic.npz")
+    return z, [str(n) for n in z["names"]]
+
+
+@pytest.mark.parametrize("name", ["kitti_max", "kitti_ign0", "topk_diff", "no_threshold", "base_yaml", "resized"])
+def test_panoptic_head_oracle(name):
+    """oracle/panoptic.py == the reference compute_pq method's cleaned_pred (panoptic.npz)."""
+    from oracle import panoptic as opan
+    z, _ = _panoptic_cases()
+    logits = torch.from_numpy(z[f"{name}__logits"].astype(np.float32))
+    mth, cth, oth, ign, thr, mode, Hi, Wi, h, w, rows = z[f"{name}__cfg"].tolist()
+    kw = dict(mask_th=mth, count_th=int(cth), overlap_th=oth, ignore_label=int(ign), threshold_output=bool(thr),
+              threshold_mode={1: "max", 2: "topk_diff"}[int(mode)])
+    B = logits.shape[0]
+    pad = torch.zeros(B, int(Hi), int(Wi), dtype=torch.bool)
+    pad[:, :int(rows), :] = True
+    got = opan.postprocess(logits, (int(Hi), int(Wi)), pad, [(int(h), int(w))] * B, **kw)
+    exp = z[f"{name}__cleaned"].astype(np.int64)
+    for i in range(B):
+        np.testing.assert_array_equal(got[i], exp[i])

@@ -66,6 +66,16 @@ def ln_case(rows, C):
     return (lambda: K.layer_norm(x, gam, bet, 1e-5)), None, 2 * x.numel() * 2
 
 
+def panoptic_case(B, Kc, H, W):
+    x = torch.randn(B, Kc, H, W, device=DEV)
+
+    def run():
+        pred, cnt, mc = K.panoptic_pixels(x, 0.5, 255, "max")
+        return K.panoptic_finalize(pred, cnt, mc, 512, 0.5, 255)
+    # two reads of the logits + pred write/read + out write
+    return run, None, 2 * x.numel() * 4 + 3 * B * H * W * 4
+
+
 CASES = {
     "conv3_l0_320": lambda: conv_case(8, 64, 64, 320, 320, temb=True, stats=True),
     "conv3_l1_640": lambda: conv_case(8, 32, 32, 640, 640, temb=True, stats=True),
@@ -101,6 +111,8 @@ CASES = {
     "gn_l0_fused": lambda: gn_case(8, 4096, 320, True),
     "gn_l0_unfused": lambda: gn_case(8, 4096, 320, False),
     "ln_l0": lambda: ln_case(32768, 320),
+    "panoptic_k128_512": lambda: panoptic_case(8, 128, 512, 512),
+    "panoptic_k30_512": lambda: panoptic_case(8, 30, 512, 512),
     "ln_l1": lambda: ln_case(8192, 640),
     "ln_l2": lambda: ln_case(2048, 1280),
 }

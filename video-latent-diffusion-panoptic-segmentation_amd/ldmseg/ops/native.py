@@ -25,6 +25,7 @@ _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _f = ctypes.c_float
 _i64 = ctypes.c_int64
+_d = ctypes.c_double
 
 
 class ConvParams(ctypes.Structure):
@@ -89,6 +90,8 @@ EXPORTS = {
     "ldm_mse_loss": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp]),
     "ldm_sq_norm": (_i, [_vp, _i64, _vp, _i, _vp]),
     "ldm_adamw": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i64, _f, _f, _f, _i, _vp, _f, _vp]),
+    "ldm_panoptic_pixels": (_i, [_vp, _i, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp]),
+    "ldm_panoptic_finalize": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _d, _i, _vp, _vp, _vp]),
     "ldm_status_string": (ctypes.c_char_p, [_i]),
     "ldm_abi_version": (_i, []),
 }
@@ -512,6 +515,46 @@ def bit_decode(planes, drop_31=True):
     _check(lib.ldm_bit_decode(_ptr(planes), batch, n, H * W, int(drop_31), _ptr(ids), dtype_code(planes.dtype),
                               _stream(planes)), "ldm_bit_decode")
     return ids
+
+
+CONF_MODE = {"none": 0, "max": 1, "topk_diff": 2}
+
+
+def panoptic_pixels(logits, mask_th, ignore_label, conf_mode="max"):
+    """logits fp32 NCHW [B, K, H, W] (GPU) -> (pred int32 [B, H, W], counts int32 [B, K],
+    mask_counts int32 [B, K]) — argmax + confidence threshold + the per-label histograms."""
+    lib = load_library()
+    _gpu(logits)
+    if logits.dtype != torch.float32 or logits.ndim != 4:
+        raise TypeError("panoptic_pixels: logits must be fp32 [B, K, H, W]")
+    logits = logits.contiguous()
+    B, Kc, H, W = logits.shape
+    dev = logits.device
+    pred = torch.empty(B, H, W, dtype=torch.int32, device=dev)
+    counts = torch.empty(B, Kc, dtype=torch.int32, device=dev)
+    mcounts = torch.empty(B, Kc, dtype=torch.int32, device=dev)
+    _check(lib.ldm_panoptic_pixels(_ptr(logits), B, Kc, H * W, CONF_MODE[conf_mode], float(mask_th), int(ignore_label),
+                                   _ptr(pred), _ptr(counts), _ptr(mcounts), _stream(logits)), "ldm_panoptic_pixels")
+    return pred, counts, mcounts
+
+
+def panoptic_finalize(pred, counts, mask_counts, count_th, overlap_th, ignore_label):
+    """-> (panoptic int32 [B, H, W] = cleaned_pred + 1, keep int32 [B, K])."""
+    lib = load_library()
+    for t in (pred, counts, mask_counts):
+        _gpu(t)
+        if t.dtype != torch.int32 or not t.is_contiguous():
+            raise TypeError("panoptic_finalize: int32 contiguous tensors expected")
+    B, H, W = pred.shape
+    Kc = counts.shape[1]
+    if counts.shape != (B, Kc) or mask_counts.shape != (B, Kc):
+        raise ValueError("panoptic_finalize: counts must be [B, K]")
+    out = torch.empty_like(pred)
+    keep = torch.empty_like(counts)
+    _check(lib.ldm_panoptic_finalize(_ptr(pred), _ptr(counts), _ptr(mask_counts), B, Kc, H * W, int(count_th),
+                                     float(overlap_th), int(ignore_label), _ptr(keep), _ptr(out), _stream(pred)),
+           "ldm_panoptic_finalize")
+    return out, keep
 
 
 def nchw_to_nhwc(sources, c_pad, dtype):
