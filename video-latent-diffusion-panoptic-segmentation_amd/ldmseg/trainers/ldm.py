@@ -118,6 +118,70 @@ class LDMTrainStep:
             s[2] = lr
         self._upload_segments()
 
+    # ---- optimizer state in torch.optim.AdamW's format (checkpoint layout, utils/checkpoint.py)
+    def reference_param_groups(self):
+        """get_optim_unet's parameter groups (trainers/optim.py:196-217 + reduce_param_groups):
+        parameters in named_modules order, grouped by their (lr, weight_decay) in order of first
+        appearance.  Returns [((lr, wd), [param, ...]), ...]."""
+        memo, groups = set(), {}
+        for _, m in self.unet.named_modules():
+            for _, q in m.named_parameters(recurse=False):
+                if not q.requires_grad or id(q) in memo or id(q) not in self.flat.index:
+                    continue
+                memo.add(id(q))
+                _, _, lr, wd = self.seg_hp[self.flat.index[id(q)]]
+                groups.setdefault((lr, wd), []).append(q)
+        return list(groups.items())
+
+    def _group_defaults(self, lr, wd):
+        g = torch.optim.AdamW([torch.zeros(1)], lr=lr, betas=self.betas, eps=self.eps, weight_decay=wd)
+        d = dict(g.param_groups[0])
+        d.pop("params")
+        return d
+
+    def state_dict(self):
+        """torch.optim.AdamW.state_dict() of the same optimizer (fp32 moments, ``step``)."""
+        state, pgs, idx = {}, [], 0
+        for (lr, wd), ps in self.reference_param_groups():
+            ids = []
+            for q in ps:
+                if self.step_count > 0:
+                    state[idx] = {"step": torch.tensor(float(self.step_count)),
+                                  "exp_avg": self.flat.view_of(q, self.exp_avg).detach().clone(),
+                                  "exp_avg_sq": self.flat.view_of(q, self.exp_avg_sq).detach().clone()}
+                ids.append(idx)
+                idx += 1
+            pgs.append({**self._group_defaults(lr, wd), "params": ids})
+        return {"state": state, "param_groups": pgs}
+
+    def load_state_dict(self, sd):
+        """Inverse of state_dict(); also accepts a reference run's AdamW state_dict when its
+        parameter grouping matches (same lr factors / weight decays)."""
+        groups = self.reference_param_groups()
+        if len(groups) != len(sd["param_groups"]):
+            raise ValueError(f"optimizer has {len(groups)} parameter groups, checkpoint {len(sd['param_groups'])}")
+        steps = set()
+        for ((_, _), ps), g in zip(groups, sd["param_groups"]):
+            if len(ps) != len(g["params"]):
+                raise ValueError("parameter group sizes differ from the checkpoint's")
+            for q, i in zip(ps, g["params"]):
+                st = sd["state"].get(i, sd["state"].get(str(i)))
+                seg = self.seg_hp[self.flat.index[id(q)]]
+                seg[2], seg[3] = float(g["lr"]), float(g["weight_decay"])
+                if st is None:
+                    self.flat.view_of(q, self.exp_avg).zero_()
+                    self.flat.view_of(q, self.exp_avg_sq).zero_()
+                    continue
+                if tuple(st["exp_avg"].shape) != tuple(q.shape):
+                    raise ValueError("optimizer state shape differs from the parameter's")
+                self.flat.view_of(q, self.exp_avg).copy_(st["exp_avg"])
+                self.flat.view_of(q, self.exp_avg_sq).copy_(st["exp_avg_sq"])
+                steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            raise ValueError("per-parameter step counts differ; the fused AdamW keeps one count")
+        self.step_count = steps.pop() if steps else 0
+        self._upload_segments()
+
     def _sink(self, p):
         return self.flat.view_of(p, self.flat.grad), False
 
