@@ -30,7 +30,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 FAMILIES = [
     ("igemm", r"igemm_kernel<", True),
     ("igemm", r"splitk_epilogue_kernel<", False),
-    ("attention", r"attn_kernel<", True),
+    ("attention", r"attn(32)?_kernel<", True),
     ("group_norm", r"gn_apply", True),
     ("group_norm", r"gn_(partial|finalize)", False),
     ("layer_norm", r"ln_kernel<", True),
