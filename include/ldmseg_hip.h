@@ -80,6 +80,8 @@ typedef struct {
   int64_t workspace_bytes;
   float* gn_partial;       /* optional: per 64-row chunk, per channel (sum, sumsq) of the output,
                               [M/64][n] float2 — the GroupNorm statistics input (NHWC, M % 64 == 0) */
+  int pad_mode;            /* 0: zero padding ksize/2 on every side; 1: diffusers Downsample2D(padding=0):
+                              F.pad (0, 1, 0, 1) then an unpadded conv (AutoencoderKL encoder) */
 } ldm_conv_params;
 
 /* Deep-K / few-tile shapes are split over K into an fp32 slab; this returns its size (0: none). */
@@ -202,6 +204,16 @@ int ldm_bit_encode(const int64_t* ids, int batch, int64_t hw, int n, int64_t ign
                    float fill_value, float* planes, uint8_t* ignore_mask, ldm_stream_t stream);
 int ldm_bit_decode(const void* planes, int batch, int n, int64_t hw, int drop_31, int64_t* ids,
                    int dtype, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * ldm_softmax_rows — p[r][j] = softmax_j(scale * s[r][j]) over the first n of `stride` columns
+ * (fp32 in, fp32 math — diffusers upcast_softmax), written with zeros in columns [n, stride) so
+ * p can be the K-padded A operand of the following P.V GEMM.  Replaces the softmax of the
+ * AutoencoderKL mid-block attention (single head, head_dim 512 > the flash kernel's 160).
+ * n <= 8192.
+ * ------------------------------------------------------------------------------------- */
+int ldm_softmax_rows(const float* s, int rows, int n, int stride, float scale, void* p, int dtype,
+                     ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Panoptic head (config 4 post-processing).

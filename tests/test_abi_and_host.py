@@ -168,3 +168,24 @@ def test_alias_package_imports_next_to_reference_name():
     from ldmseg_mi355x.models import GeneralVAESeg, UNet  # noqa: F401
     from ldmseg_mi355x.schedulers import DDIMNoiseScheduler  # noqa: F401
     assert m.__name__ == "ldmseg_mi355x" and UNet.__module__ == "ldmseg_mi355x.models.unet"
+
+
+def test_autoencoder_kl_structure_and_legacy_keys():
+    """GeneralVAEImage keeps diffusers' AutoencoderKL names (encoder.*, quant_conv, post_quant_conv;
+    no decoder keys, tools/main_ldm.py:139) and accepts the pre-0.14 attention names."""
+    from ldmseg.models.autoencoder_kl import GeneralVAEImage
+    m = GeneralVAEImage()
+    sd = m.state_dict()
+    n_enc = sum(v.numel() for k, v in sd.items() if k.startswith("encoder."))
+    assert n_enc == 34_163_592                      # SD-1.x VAE encoder
+    assert "encoder.mid_block.attentions.0.to_out.0.weight" in sd
+    assert "encoder.down_blocks.0.downsamplers.0.conv.weight" in sd
+    assert "encoder.down_blocks.3.downsamplers.0.conv.weight" not in sd
+    assert not any(k.startswith("decoder.") for k in sd)
+    legacy = {k.replace(".to_q.", ".query.").replace(".to_out.0.", ".proj_attn."): v.clone() for k, v in sd.items()}
+    legacy["decoder.conv_in.weight"] = torch.zeros(1)          # decoder weights of a full checkpoint are skipped
+    m2 = GeneralVAEImage()
+    m2.load_state_dict(legacy)
+    assert torch.equal(m2.encoder.mid_block.attentions[0].to_q.weight, m.encoder.mid_block.attentions[0].to_q.weight)
+    m2.set_scaling_factor(0.2)
+    assert m2.scaling_factor == 0.2

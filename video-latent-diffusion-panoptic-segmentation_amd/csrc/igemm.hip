@@ -1257,11 +1257,12 @@ int validate(const ldm_conv_params* q, int* es_out) {
   const int cin = q->c0 + q->c1;
   if (q->ksize * q->ksize * cin > q->kpad || q->n <= 0) return LDM_ERR_ARG;
   if (!aligned16(q->a0) || (q->a1 && !aligned16(q->a1)) || !aligned16(q->w)) return LDM_ERR_ALIGN;
-  const int pad = q->ksize / 2;
+  if (q->pad_mode < 0 || q->pad_mode > 1 || (q->pad_mode == 1 && (q->upsample || q->ksize != 3))) return LDM_ERR_ARG;
+  const int pad_sum = q->pad_mode == 1 ? 1 : 2 * (q->ksize / 2);   // total rows/cols of zero padding
   const int hin_eff = q->upsample ? 2 * q->h_in : q->h_in;
   const int win_eff = q->upsample ? 2 * q->w_in : q->w_in;
-  if (q->h_out != (hin_eff + 2 * pad - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
-  if (q->w_out != (win_eff + 2 * pad - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
+  if (q->h_out != (hin_eff + pad_sum - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
+  if (q->w_out != (win_eff + pad_sum - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
   if (q->out_layout == LDM_OUT_GEGLU && (q->n % 32 || q->residual || q->temb || q->gn_partial)) return LDM_ERR_ARG;
   if (q->out_layout == LDM_OUT_SHUFFLE2 && (q->n % 16 || q->temb || q->upsample)) return LDM_ERR_ARG;
   if (q->out_layout < 0 || q->out_layout > 3) return LDM_ERR_ARG;
@@ -1325,7 +1326,7 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.c0 = q->c0; a.c1 = q->c1; a.cin = cin;
   a.h_in = q->h_in; a.w_in = q->w_in;
   a.h_out = q->h_out; a.w_out = q->w_out; a.hw_out = q->h_out * q->w_out;
-  a.ksize = q->ksize; a.stride = q->stride; a.upsample = q->upsample; a.pad = q->ksize / 2;
+  a.ksize = q->ksize; a.stride = q->stride; a.upsample = q->upsample; a.pad = q->pad_mode == 1 ? 0 : q->ksize / 2;
   a.w = static_cast<const char*>(q->w);
   a.w_bytes = (int)((int64_t)q->n * q->kpad * es);
   a.n = q->n; a.kpad = q->kpad; a.K = q->ksize * q->ksize * cin;

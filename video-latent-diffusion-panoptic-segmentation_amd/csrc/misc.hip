@@ -318,3 +318,67 @@ extern "C" const char* ldm_status_string(int status) {
 }
 
 extern "C" int ldm_abi_version(void) { return 1; }
+
+// ---------------------------------------------------------------------------------------
+// ldm_softmax_rows: one wave per row, the row held in registers (<= 128 values per lane), fp32
+// max / exp / sum, output bf16 or fp32 with zero fill of the padding columns.
+// ---------------------------------------------------------------------------------------
+namespace {
+template <typename T, int VPL>
+__global__ __launch_bounds__(256) void softmax_rows_kernel(const float* __restrict__ s, int rows, int n, int stride,
+                                                           float scale, T* __restrict__ p) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* sr = s + (int64_t)row * stride;
+  float v[VPL];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int j = lane + 64 * i;
+    v[i] = j < n ? sr[j] * scale : -INFINITY;
+    m = fmaxf(m, v[i]);
+  }
+  m = wave_max(m);
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    v[i] = lane + 64 * i < n ? __expf(v[i] - m) : 0.f;
+    sum += v[i];
+  }
+  const float inv = 1.0f / wave_sum(sum);
+  T* pr = p + (int64_t)row * stride;
+#pragma unroll
+  for (int i = 0; i < VPL; ++i) {
+    const int j = lane + 64 * i;
+    if (j < stride) pr[j] = from_f<T>(v[i] * inv);
+  }
+}
+
+template <typename T>
+int softmax_launch(const float* s, int rows, int n, int stride, float scale, void* p, hipStream_t st) {
+  const int vpl = (stride + 63) / 64;
+  const dim3 grid((rows + 3) / 4);
+#define SM_CASE(V)                                                                                        \
+  if (vpl <= V) {                                                                                         \
+    hipLaunchKernelGGL((softmax_rows_kernel<T, V>), grid, dim3(256), 0, st, s, rows, n, stride, scale,   \
+                       static_cast<T*>(p));                                                               \
+    return LDM_OK;                                                                                        \
+  }
+  SM_CASE(4) SM_CASE(16) SM_CASE(64) SM_CASE(128)
+#undef SM_CASE
+  return LDM_ERR_ARG;
+}
+}  // namespace
+
+extern "C" int ldm_softmax_rows(const float* s, int rows, int n, int stride, float scale, void* p, int dtype,
+                                ldm_stream_t stream) {
+  if (!s || !p || rows <= 0 || n <= 0 || stride < n || stride > 8192) return LDM_ERR_ARG;
+  if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int r = dtype == LDM_BF16 ? softmax_launch<bf16_t>(s, rows, n, stride, scale, p, st)
+                                  : softmax_launch<float>(s, rows, n, stride, scale, p, st);
+  if (r != LDM_OK) return r;
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}

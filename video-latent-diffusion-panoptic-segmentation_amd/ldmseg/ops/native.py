@@ -33,7 +33,7 @@ class ConvParams(ctypes.Structure):
                 ("h_out", _i), ("w_out", _i), ("ksize", _i), ("stride", _i), ("upsample", _i), ("w", _vp),
                 ("n", _i), ("kpad", _i), ("bias", _vp), ("temb", _vp), ("temb_stride", _i), ("residual", _vp),
                 ("out", _vp), ("out_layout", _i), ("act", _i), ("dtype", _i), ("out_f32", _i),
-                ("workspace", _vp), ("workspace_bytes", _i64), ("gn_partial", _vp)]
+                ("workspace", _vp), ("workspace_bytes", _i64), ("gn_partial", _vp), ("pad_mode", _i)]
 
 
 class AttnParams(ctypes.Structure):
@@ -92,6 +92,7 @@ EXPORTS = {
     "ldm_adamw": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i64, _f, _f, _f, _i, _vp, _f, _vp]),
     "ldm_panoptic_pixels": (_i, [_vp, _i, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp]),
     "ldm_panoptic_finalize": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _d, _i, _vp, _vp, _vp]),
+    "ldm_softmax_rows": (_i, [_vp, _i, _i, _i, _f, _vp, _i, _vp]),
     "ldm_status_string": (ctypes.c_char_p, [_i]),
     "ldm_abi_version": (_i, []),
 }
@@ -254,6 +255,18 @@ class PackedConv:
         self.shuffle2 = shuffle2
 
 
+def packed_rows(t, bias=None):
+    """Wrap a contiguous [n][k] activation tensor (k % 64 == 0) as the B operand of a 1x1
+    ldm_conv2d without copying: out[m, j] = sum_k A[m, k] * t[j, k] (+ bias[j])."""
+    if t.ndim != 2 or not t.is_contiguous() or t.shape[1] % 64:
+        raise ValueError("packed_rows: need a contiguous [n, k] tensor with k % 64 == 0")
+    pc = PackedConv.__new__(PackedConv)
+    pc.ksize, pc.cin, pc.cin_real, pc.n, pc.kpad = 1, t.shape[1], t.shape[1], t.shape[0], t.shape[1]
+    pc.w, pc.dtype, pc.geglu, pc.shuffle2 = t, t.dtype, False, False
+    pc.bias = None if bias is None else bias.detach().float().contiguous()
+    return pc
+
+
 GN_PART_ATTR = "_ldm_gn_part"
 
 
@@ -263,7 +276,7 @@ def gn_stats_of(t):
 
 
 def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False, temb=None, temb_stride=0,
-           residual=None, out=None, out_layout=OUT_NHWC, act=ACT_NONE, out_dtype=None, gn_stats=False):
+           residual=None, out=None, out_layout=OUT_NHWC, act=ACT_NONE, out_dtype=None, gn_stats=False, pad_mode=0):
     """Run ldm_conv2d.  x0/x1: NHWC [batch, h, w, c] (any contiguous view with that numel).
 
     gn_stats=True also has the epilogue write per-64-row-chunk channel (sum, sumsq) of the
@@ -284,6 +297,8 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
         ho, wo = h, w
     elif upsample:
         ho, wo = 2 * h, 2 * w
+    elif pad_mode == 1:                    # diffusers Downsample2D(padding=0): F.pad (0, 1, 0, 1)
+        ho, wo = (h + 1 - 3) // stride + 1, (w + 1 - 3) // stride + 1
     else:
         ho, wo = (h + 2 - 3) // stride + 1, (w + 2 - 3) // stride + 1
     n = pc.n
@@ -316,7 +331,7 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
     p = ConvParams(_ptr(x0), _ptr(x1), c0, c1, batch, h, w, ho, wo, pc.ksize, stride, int(upsample), _ptr(pc.w),
                    n, pc.kpad, _ptr(pc.bias), _ptr(temb), temb_stride, _ptr(residual), _ptr(out), out_layout, act,
                    dtype_code(pc.dtype), int(odt == torch.float32 and pc.dtype != torch.float32), None, 0,
-                   _ptr(part))
+                   _ptr(part), int(pad_mode))
     ws_bytes = int(lib.ldm_conv2d_workspace_bytes(ctypes.byref(p)))
     if ws_bytes:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x0.device)
@@ -332,6 +347,20 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
               f"Cin={c0}+{c1} L{out_layout}"
         _prof_stop(ev, "igemm", flops, nbytes, det)
     return out
+
+
+def softmax_rows(s, n, scale, dtype):
+    """s fp32 [rows, stride] (GPU) -> softmax over the first n columns of scale * s, zeros in
+    columns [n, stride); output dtype fp32 or bf16."""
+    lib = load_library()
+    _gpu(s)
+    if s.dtype != torch.float32 or s.ndim != 2 or not s.is_contiguous():
+        raise TypeError("softmax_rows: s must be a contiguous fp32 [rows, stride] tensor")
+    rows, stride = s.shape
+    p = torch.empty(rows, stride, dtype=dtype, device=s.device)
+    _check(lib.ldm_softmax_rows(_ptr(s), rows, int(n), stride, float(scale), _ptr(p), dtype_code(dtype), _stream(s)),
+           "ldm_softmax_rows")
+    return p
 
 
 def force_attention_legacy(legacy=True):
