@@ -151,12 +151,15 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=2)
-    ap.add_argument("--mode", default="denoise", choices=["denoise", "train"],
-                    help="denoise: the headline metric; train: config 3's DDP training iteration")
+    ap.add_argument("--mode", default="denoise", choices=["denoise", "train", "sample"],
+                    help="denoise: the headline metric; train: config 3's DDP training iteration; "
+                         "sample: config 4's full clip sampling (encode -> 50 DDIM steps -> decode -> panoptic)")
     ap.add_argument("--clips", type=int, default=2, help="train mode: clips of T frames per GPU")
     args = ap.parse_args()
     if args.mode == "train":
         return main_train(args)
+    if args.mode == "sample":
+        return main_sample(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -213,6 +216,65 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+SAMPLE_METRIC = "full panoptic sampling clips/sec (T=8 KITTI frames 192x640, 50 DDIM steps, K=128)"
+
+
+def main_sample(args):
+    """Config 4: per clip, RGB encode (SD VAE encoder at 192x192) -> 50 DDIM steps of the UNet ->
+    seg-VAE decode to K=128 logits at 512x512 -> resize to the frame -> panoptic head.  `steps`
+    clips are timed after `warmup` untimed clips; every rank samples its own clips."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    from ldmseg.models import GeneralVAESeg
+    from ldmseg.models.autoencoder_kl import GeneralVAEImage
+    from ldmseg.pipelines import DenoiseStep
+    from ldmseg.pipelines.sample import sample_panoptic
+    from ldmseg.utils import max_over_ranks
+    torch.manual_seed(0)
+    unet = build_unet(dev, dtype)
+    sched = make_scheduler(dev)
+    vae_image = GeneralVAEImage().to(dev, dtype).eval()
+    vae_seg = GeneralVAESeg(in_channels=16, int_channels=256, out_channels=128, block_out_channels=(32, 64, 128, 256),
+                            num_upscalers=2, scaling_factor=0.2).to(dev, dtype).eval()
+    B, L = args.frames, args.latent
+    steps = args.steps if args.steps != 20 else 3        # default: 3 timed clips
+    warm = min(args.warmup, 1)
+    g = torch.Generator().manual_seed(1 + rank)
+    clip = torch.rand(B, 3, 192, 640, generator=g).to(dev)
+    stepper = DenoiseStep(unet, sched, torch.zeros(B, 4, L, L, device=dev), self_condition=False,
+                          use_graph=not args.no_graph)
+    run = lambda: sample_panoptic(clip, vae_image, vae_seg, unet, sched, latent_size=L, stepper=stepper)  # noqa
+    for _ in range(warm):
+        run()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res = run()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
+    if rank == 0:
+        print(json.dumps({
+            "metric": SAMPLE_METRIC, "value": round(world * steps / elapsed, 4), "unit": "clips/s", "n_gpus": world,
+            "steps": steps, "warmup": warm, "ms_per_step": round(elapsed / steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic: random-init SD-1.4 UNet / SD VAE encoder / seg-VAE (K=128) weights, U(0,1) frames",
+            "config": {"workload": f"clip of T={B} frames: encode + 50 DDIM steps + decode + panoptic head",
+                       "global_batch": B * world, "parallelism": f"replicas x{world}"},
+            "segments_frame0": len(res[0]["panoptic_seg"][1])}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
