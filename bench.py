@@ -151,15 +151,18 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=2)
-    ap.add_argument("--mode", default="denoise", choices=["denoise", "train", "sample"],
+    ap.add_argument("--mode", default="denoise", choices=["denoise", "train", "sample", "ae"],
                     help="denoise: the headline metric; train: config 3's DDP training iteration; "
-                         "sample: config 4's full clip sampling (encode -> 50 DDIM steps -> decode -> panoptic)")
+                         "sample: config 4's full clip sampling (encode -> 50 DDIM steps -> decode -> panoptic); "
+                         "ae: config 1's VAE (autoencoder) training iteration")
     ap.add_argument("--clips", type=int, default=2, help="train mode: clips of T frames per GPU")
     args = ap.parse_args()
     if args.mode == "train":
         return main_train(args)
     if args.mode == "sample":
         return main_sample(args)
+    if args.mode == "ae":
+        return main_ae(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -277,6 +280,46 @@ def main_sample(args):
             "segments_frame0": len(res[0]["panoptic_seg"][1])}), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+AE_METRIC = "VAE (autoencoder) training iterations/sec (4 semKITTI frames 10x192x640, point losses)"
+
+
+def main_ae(args):
+    """Config 1 (main_worker_ae.py): GeneralVAESeg (KITTI: 10 bits in, 30 classes out) train
+    iteration on 4 synthetic frames: forward with posterior sampling, CE + BCE/dice point losses
+    (12544 points, oversample 3), backward, clip 3.0, AdamW."""
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    from ldmseg.models import GeneralVAESeg
+    from ldmseg.trainers.ae import AETrainStep
+    torch.manual_seed(0)
+    vae = GeneralVAESeg(in_channels=10, int_channels=256, out_channels=30, block_out_channels=(32, 64, 128, 256),
+                        num_upscalers=2, scaling_factor=0.2).to(dev, dtype).train()
+    g = torch.Generator().manual_seed(1)
+    lo = torch.randn(4, 20, 12, 40, generator=g)
+    targets = torch.nn.functional.interpolate(lo, size=(192, 640), mode="bilinear").argmax(1).to(dev)
+    bits = torch.stack([(targets >> i) & 1 for i in range(5)] * 2, 1).float()
+    st = AETrainStep(vae, lr=1e-4, clip_grad=3.0, ignore_label=0)
+    steps = args.steps
+    for _ in range(args.warmup):
+        st.train_step(bits, targets)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        loss, ce, mask = st.train_step(bits, targets)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": AE_METRIC, "value": round(steps / elapsed, 4), "unit": "iterations/s", "n_gpus": 1,
+        "steps": steps, "warmup": args.warmup, "ms_per_step": round(elapsed / steps * 1e3, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+        "data": "synthetic: blobby 20-class KITTI-shaped targets, their 5+5 bit planes; random-init VAE (1.80 M)",
+        "config": {"workload": "AE train iteration, B=4 frames 192x640", "global_batch": 4},
+        "loss": round(loss.item(), 5), "reference_cpu_s_per_iter": "0.93-1.31 (8 CPU cores, SURVEY.md §6)"}),
+        flush=True)
 
 
 TRAIN_METRIC = "LDM training iterations/sec (2 clips x T=8 per GPU, 4x64x64 latents, self-conditioning)"

@@ -216,6 +216,49 @@ int ldm_softmax_rows(const float* s, int rows, int n, int stride, float scale, v
                      ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * AE training (row a16): the point losses of SegmentationLosses.point_loss
+ * (ldmseg/trainers/losses.py:117-395, detectron2_utils.py:20-100) and VAE-backward helpers.
+ * A "box" is one image (C planes, planes == NULL) or one mask (the single plane planes[box]).
+ * coords: [boxes][p] float2 in [0, 1]^2 (x, y), as point_sample takes them.
+ * ldm_point_sample:      out[box][c][p] = grid_sample(bilinear, zeros, align_corners=False).
+ * ldm_point_sample_bwd:  din += adjoint (atomic), point gradients scaled by scale * *scale_ptr.
+ * ldm_point_labels:      mode 0: int64 labels by nearest sampling of targets [img][h][w] (zeros
+ *                        padding); mode 1: fp32 bilinear sample of (targets[img[box]] == cls[box]).
+ * ldm_point_uncertainty: u = top2[1] - top2[0] over c (c > 1) or -|x| (c == 1).
+ * ldm_topk_select:       idx[row][k] = indices of the k largest u[row][:n] (ties at the k-th value in
+ *                        index order; the set, not the order, is specified); coords_out[row][k] the
+ *                        gathered coords (optional).
+ * ldm_point_ce:          acc = (sum of CE over non-ignored points, their count) as doubles; grad =
+ *                        (softmax(x / T) - onehot) / T (0 at ignored points), unscaled by the count.
+ * ldm_point_bce_dice:    acc = (sum over masks of mean BCE, sum of dice); grad = d(bce_mean + dice)/dx.
+ * ldm_silu:              out = silu(z) (dy == NULL) or dy * silu'(z).
+ * ldm_space_to_depth2:   [b][2h][2w][c] -> [b][h][w][(dy, dx, c)] (ConvTranspose k2s2 backward).
+ * ldm_posterior_sample / _bwd: z = mean + exp(clamp(logvar, -30, 20) / 2) * eps from NCHW fp32
+ *                        moments; the backward reads dz from NHWC rows of c_stride channels.
+ * ------------------------------------------------------------------------------------- */
+int ldm_point_sample(const float* in, int boxes, int c, int h, int w, const int32_t* planes, const float* coords,
+                     int p, float* out, ldm_stream_t stream);
+int ldm_point_sample_bwd(const float* dout, int boxes, int c, int h, int w, const int32_t* planes,
+                         const float* coords, int p, const float* scale_ptr, float scale, float* din,
+                         ldm_stream_t stream);
+int ldm_point_labels(const int64_t* targets, int h, int w, const int32_t* img, const int32_t* cls,
+                     const float* coords, int boxes, int p, int mode, int64_t* labels, float* values,
+                     ldm_stream_t stream);
+int ldm_point_uncertainty(const float* x, int boxes, int c, int p, float* u, ldm_stream_t stream);
+int ldm_topk_select(const float* u, int rows, int n, int k, const float* coords, int32_t* idx, float* coords_out,
+                    ldm_stream_t stream);
+int ldm_point_ce(const float* x, const int64_t* labels, int boxes, int c, int p, float temperature,
+                 int64_t ignore_label, double* acc, float* grad, ldm_stream_t stream);
+int ldm_point_bce_dice(const float* x, const float* y, int masks, int p, double* acc, float* grad,
+                       ldm_stream_t stream);
+int ldm_silu(const void* z, const void* dy, int64_t n, void* out, int dtype, ldm_stream_t stream);
+int ldm_space_to_depth2(const void* d, int batch, int h, int w, int c, void* out, int dtype, ldm_stream_t stream);
+int ldm_posterior_sample(const float* moments, const float* eps, int batch, int latent, int hw, float* z,
+                         ldm_stream_t stream);
+int ldm_posterior_bwd(const float* moments, const float* eps, const void* dz, int c_stride, int batch, int latent,
+                      int hw, float* dmoments, int dtype, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * Panoptic head (config 4 post-processing).
  * Replaces: the per-image CPU loop of TrainerDiffusion.compute_pq
  * (ldmseg/trainers/trainers_ldm_cond.py:1287-1330) and the argmax / confidence threshold of

@@ -11,6 +11,10 @@ What is pinned (each array is data: inputs + the reference's outputs):
   ddim.npz   DDIMNoiseScheduler       ldmseg/schedulers/ddim_scheduler.py:32-269
   vae.npz    GeneralVAESeg            ldmseg/models/vae.py:42-323 (gaussian, no mid blocks)
   vpq.npz    eval_dvpq.vpq_eval       eval/eval_dvpq.py:25-101
+  ae.npz     one AE training iteration's loss and parameter gradients: the reference
+             GeneralVAESeg (train mode, sample_posterior=True) + SegmentationLosses.point_loss
+             (trainers_ae.py:321-331, losses.py:117-395), torch.rand / torch.randn drawn from
+             seeded CPU generators in call order (the GPU test replays the same draws)
   panoptic.npz  TrainerDiffusion.compute_pq's per-image panoptic head
              ldmseg/trainers/trainers_ldm_cond.py:1185-1330, run as the reference method on a
              stand-in trainer whose sample/decode_latents return seeded logits; the
@@ -378,6 +382,94 @@ def gen_panoptic():
     print("panoptic.npz:", len(out), "arrays")
 
 
+# --------------------------------------------------------------------------------------
+# AE training iteration (config 1): reference VAE forward + point losses + backward
+# --------------------------------------------------------------------------------------
+AE_CFG = dict(in_channels=10, int_channels=64, out_channels=30, block_out_channels=(16, 32, 32, 64),
+              latent_channels=4, num_latents=2, num_upscalers=2, upscale_channels=64, norm_num_groups=16,
+              scaling_factor=0.2, parametrization="gaussian", num_mid_blocks=0, act_fn="none", clamp_output=False)
+AE_SEEDS = (123, 456)          # torch.rand / torch.randn replay generators
+
+
+class _Replay:
+    """torch.rand / torch.randn replaced by draws from seeded CPU generators (then moved)."""
+
+    def __init__(self):
+        self.g_rand = torch.Generator().manual_seed(AE_SEEDS[0])
+        self.g_randn = torch.Generator().manual_seed(AE_SEEDS[1])
+        self.orig = (torch.rand, torch.randn)
+
+    def rand(self, *size, device=None, **kw):
+        size = size[0] if len(size) == 1 and isinstance(size[0], (tuple, list, torch.Size)) else size
+        return self.orig[0](*size, generator=self.g_rand).to(device or "cpu")
+
+    def randn(self, *size, generator=None, device=None, dtype=None, **kw):
+        size = size[0] if len(size) == 1 and isinstance(size[0], (tuple, list, torch.Size)) else size
+        return self.orig[1](*size, generator=self.g_randn).to(device or "cpu", dtype or torch.float32)
+
+    def topk(self, x, k, *a, **kw):
+        r = self.orig_topk(x, k, *a, **kw)
+        if k > 2:                                   # the point selection, not calculate_uncertainty_seg
+            self.selected.append(r[1].clone())
+        return r
+
+    def __enter__(self):
+        self.selected = []
+        self.orig_topk = torch.topk
+        torch.rand, torch.randn, torch.topk = self.rand, self.randn, self.topk
+        return self
+
+    def __exit__(self, *a):
+        torch.rand, torch.randn = self.orig
+        torch.topk = self.orig_topk
+
+
+def _blob_labels(gen, B, H, W, n_cls, cell=16):
+    lo = torch.randn(B, n_cls, max(2, H // cell), max(2, W // cell), generator=gen)
+    return torch.nn.functional.interpolate(lo, size=(H, W), mode="bilinear", align_corners=False).argmax(1)
+
+
+def gen_ae():
+    from ldmseg.models.vae import GeneralVAESeg
+    from ldmseg.trainers.losses import SegmentationLosses
+
+    torch.manual_seed(0)
+    model = GeneralVAESeg(**AE_CFG, encoder=None).train()
+    gen = torch.Generator().manual_seed(21)
+    q = _quantized_init(model, gen)
+    out = {}
+    for name, (qi, scale, plus_one) in q.items():
+        out[f"w__{name}__q"] = qi
+        out[f"w__{name}__scale"] = scale
+        out[f"w__{name}__plus1"] = np.bool_(plus_one)
+    B, H, W = 2, 64, 160
+    targets = _blob_labels(gen, B, H, W, 12)                       # classes 0..11, 0 = ignore_label
+    ids = targets.clone()
+    bits = torch.stack([(ids >> i) & 1 for i in range(5)] + [(ids >> i) & 1 for i in range(5)], 1).float()
+    images = 2.0 * bits - 1.0                                       # trainers_ae.py:294-295
+    losses = SegmentationLosses(num_points=12544, oversample_ratio=3, importance_sample_ratio=0.75,
+                                ignore_label=0, temperature=1.0)
+    with _Replay() as rp:
+        output = model(images, sample_posterior=True)
+        ls = losses.point_loss(output.sample, targets)
+    # the reference's uncertain-point indices (CE boxes, then mask boxes), uint16 (< 37632)
+    out["sel_ce"] = rp.selected[0].numpy().astype(np.uint16)
+    out["sel_mask"] = rp.selected[1].numpy().astype(np.uint16)
+    kl = torch.mean(output.posterior.kl())
+    total = 1.0 * ls["ce"] + 1.0 * ls["mask"] + 0.0 * kl             # base.yaml loss_weights
+    total.backward()
+    out["bits"] = bits.numpy().astype(np.uint8)
+    out["targets"] = targets.numpy().astype(np.int16)
+    out["ce"] = np.float64(ls["ce"].item())
+    out["mask"] = np.float64(ls["mask"].item())
+    out["loss"] = np.float64(total.item())
+    for name, p in model.named_parameters():
+        out[f"g__{name}"] = p.grad.numpy().astype(np.float32)
+    out["names"] = np.array([n for n, _ in model.named_parameters()])
+    np.savez_compressed(os.path.join(HERE, "ae.npz"), **out)
+    print("ae.npz:", len(out), "arrays", "ce", out["ce"], "mask", out["mask"])
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     gen_codec()
@@ -385,3 +477,4 @@ if __name__ == "__main__":
     gen_vae()
     gen_vpq()
     gen_panoptic()
+    gen_ae()

@@ -118,3 +118,32 @@ def test_panoptic_head_oracle(name):
     exp = z[f"{name}__cleaned"].astype(np.int64)
     for i in range(B):
         np.testing.assert_array_equal(got[i], exp[i])
+
+
+def test_ae_iteration_oracle():
+    """oracle/ae.py (autograd over the restated VAE + point losses) == the reference's AE iteration
+    (ae.npz) with the reference's draws replayed and its point selection forced."""
+    from oracle import ae as oae
+    z = load("ae.npz")
+    cfg = dict(in_channels=10, int_channels=64, out_channels=30, block_out_channels=(16, 32, 32, 64),
+               latent_channels=4, num_latents=2, num_upscalers=2, norm_num_groups=16)
+    sd = {}
+    for name in z["names"]:
+        name = str(name)
+        v = z[f"w__{name}__q"].astype(np.float32) * z[f"w__{name}__scale"]
+        if bool(z[f"w__{name}__plus1"]):
+            v = v + np.float32(1.0)
+        sd[name] = torch.from_numpy(v.astype(np.float32))
+    g_rand = torch.Generator().manual_seed(123)
+    g_randn = torch.Generator().manual_seed(456)
+    sels = [torch.from_numpy(z["sel_ce"].astype(np.int64)), torch.from_numpy(z["sel_mask"].astype(np.int64))]
+    torch.set_num_threads(8)
+    loss, ce, mask, grads = oae.train_iteration(
+        sd, cfg, torch.from_numpy(z["bits"].astype(np.float32)), torch.from_numpy(z["targets"].astype(np.int64)),
+        rand=lambda *s: torch.rand(*s, generator=g_rand), randn=lambda s: torch.randn(*s, generator=g_randn),
+        select=lambda u, k: sels.pop(0))
+    assert abs(ce.item() - float(z["ce"])) <= 1e-5 * float(z["ce"])
+    assert abs(mask.item() - float(z["mask"])) <= 1e-5 * float(z["mask"])
+    for name in z["names"]:
+        ref = torch.from_numpy(z[f"g__{name}"])
+        assert (grads[str(name)] - ref).norm() <= 1e-4 * ref.norm(), name

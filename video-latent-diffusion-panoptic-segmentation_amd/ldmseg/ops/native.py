@@ -93,6 +93,17 @@ EXPORTS = {
     "ldm_panoptic_pixels": (_i, [_vp, _i, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp]),
     "ldm_panoptic_finalize": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _d, _i, _vp, _vp, _vp]),
     "ldm_softmax_rows": (_i, [_vp, _i, _i, _i, _f, _vp, _i, _vp]),
+    "ldm_point_sample": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp]),
+    "ldm_point_sample_bwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _f, _vp, _vp]),
+    "ldm_point_labels": (_i, [_vp, _i, _i, _vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    "ldm_point_uncertainty": (_i, [_vp, _i, _i, _i, _vp, _vp]),
+    "ldm_topk_select": (_i, [_vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "ldm_point_ce": (_i, [_vp, _vp, _i, _i, _i, _f, _i64, _vp, _vp, _vp]),
+    "ldm_point_bce_dice": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
+    "ldm_silu": (_i, [_vp, _vp, _i64, _vp, _i, _vp]),
+    "ldm_space_to_depth2": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp]),
+    "ldm_posterior_sample": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp]),
+    "ldm_posterior_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _i, _vp]),
     "ldm_status_string": (ctypes.c_char_p, [_i]),
     "ldm_abi_version": (_i, []),
 }
@@ -888,3 +899,145 @@ def attention_bwd(q, k, v, o, d_o, lse, batch, heads, head_dim, n_q, n_kv, q_str
                                  dq_stride, dkv_stride, _ptr(ws), _stream(q)), "ldm_attention_bwd")
     _prof_stop(ev, "attention_bwd", 10.0 * batch * heads * n_q * n_kv * head_dim,
                (4 * batch * n_q * C + 4 * batch * n_kv * C) * q.element_size(), f"N={n_q} L={n_kv} d={head_dim}")
+
+
+# ======================================================================================
+# AE training (row a16): point losses + VAE-backward helpers
+# ======================================================================================
+def _coords(c, boxes):
+    if c.dtype != torch.float32 or c.ndim != 3 or c.shape[0] != boxes or c.shape[2] != 2 or not c.is_contiguous():
+        raise ValueError("coords must be contiguous fp32 [boxes, P, 2]")
+    return c.shape[1]
+
+
+def point_sample(x, coords, planes=None):
+    """x fp32 NCHW [N, C, H, W]; boxes = N (C planes each) or len(planes) (one plane each, index
+    into the flattened N*C planes) -> [boxes, C or 1, P]."""
+    lib = load_library()
+    _gpu(x, coords, planes)
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        raise TypeError("point_sample: x must be contiguous fp32 NCHW")
+    N, C, H, W = x.shape
+    boxes = N if planes is None else planes.numel()
+    P = _coords(coords, boxes)
+    cc = C if planes is None else 1
+    out = torch.empty(boxes, cc, P, dtype=torch.float32, device=x.device)
+    _check(lib.ldm_point_sample(_ptr(x), boxes, cc, H, W, _ptr(planes), _ptr(coords), P, _ptr(out), _stream(x)),
+           "ldm_point_sample")
+    return out
+
+
+def point_sample_bwd(dout, coords, din, planes=None, scale_t=None, scale=1.0):
+    """din (fp32 NCHW, accumulated in place) += adjoint of point_sample applied to dout * scale * scale_t."""
+    lib = load_library()
+    _gpu(dout, coords, din, planes, scale_t)
+    N, C, H, W = din.shape
+    boxes, cc, P = dout.shape
+    if _coords(coords, boxes) != P or cc != (C if planes is None else 1):
+        raise ValueError("point_sample_bwd: shapes do not match")
+    _check(lib.ldm_point_sample_bwd(_ptr(dout), boxes, cc, H, W, _ptr(planes), _ptr(coords), P, _ptr(scale_t),
+                                    float(scale), _ptr(din), _stream(din)), "ldm_point_sample_bwd")
+
+
+def point_labels_nearest(targets, coords):
+    lib = load_library()
+    _gpu(targets, coords)
+    B, H, W = targets.shape
+    P = _coords(coords, B)
+    lab = torch.empty(B, P, dtype=torch.int64, device=targets.device)
+    _check(lib.ldm_point_labels(_ptr(targets.contiguous()), H, W, None, None, _ptr(coords), B, P, 0, _ptr(lab), None,
+                                _stream(targets)), "ldm_point_labels")
+    return lab
+
+
+def point_labels_mask(targets, img, cls, coords):
+    lib = load_library()
+    _gpu(targets, img, cls, coords)
+    B, H, W = targets.shape
+    boxes = img.numel()
+    P = _coords(coords, boxes)
+    val = torch.empty(boxes, P, dtype=torch.float32, device=targets.device)
+    _check(lib.ldm_point_labels(_ptr(targets.contiguous()), H, W, _ptr(img), _ptr(cls), _ptr(coords), boxes, P, 1,
+                                None, _ptr(val), _stream(targets)), "ldm_point_labels")
+    return val
+
+
+def point_uncertainty(x):
+    lib = load_library()
+    _gpu(x)
+    boxes, C, P = x.shape
+    u = torch.empty(boxes, P, dtype=torch.float32, device=x.device)
+    _check(lib.ldm_point_uncertainty(_ptr(x), boxes, C, P, _ptr(u), _stream(x)), "ldm_point_uncertainty")
+    return u
+
+
+def topk_select(u, k, coords=None):
+    lib = load_library()
+    _gpu(u, coords)
+    rows, n = u.shape
+    idx = torch.empty(rows, k, dtype=torch.int32, device=u.device)
+    co = None if coords is None else torch.empty(rows, k, 2, dtype=torch.float32, device=u.device)
+    _check(lib.ldm_topk_select(_ptr(u.contiguous()), rows, n, k, _ptr(coords), _ptr(idx), _ptr(co), _stream(u)),
+           "ldm_topk_select")
+    return idx, co
+
+
+def point_ce(x, labels, temperature, ignore_label):
+    lib = load_library()
+    _gpu(x, labels)
+    B, C, P = x.shape
+    acc = torch.empty(2, dtype=torch.float64, device=x.device)
+    grad = torch.empty_like(x)
+    _check(lib.ldm_point_ce(_ptr(x), _ptr(labels), B, C, P, float(temperature), int(ignore_label), _ptr(acc),
+                            _ptr(grad), _stream(x)), "ldm_point_ce")
+    return acc, grad
+
+
+def point_bce_dice(x, y):
+    lib = load_library()
+    _gpu(x, y)
+    M, P = x.shape
+    acc = torch.empty(2, dtype=torch.float64, device=x.device)
+    grad = torch.empty_like(x)
+    _check(lib.ldm_point_bce_dice(_ptr(x), _ptr(y), M, P, _ptr(acc), _ptr(grad), _stream(x)), "ldm_point_bce_dice")
+    return acc, grad
+
+
+def silu(z, dy=None):
+    lib = load_library()
+    _gpu(z, dy)
+    out = torch.empty_like(z)
+    _check(lib.ldm_silu(_ptr(z), _ptr(dy), z.numel(), _ptr(out), dtype_code(z.dtype), _stream(z)), "ldm_silu")
+    return out
+
+
+def space_to_depth2(d, batch, h, w):
+    """d NHWC [batch, 2h, 2w, c] -> [batch, h, w, 4c] in (dy, dx, c) order."""
+    lib = load_library()
+    _gpu(d)
+    c = d.numel() // (batch * 4 * h * w)
+    out = torch.empty(batch, h, w, 4 * c, dtype=d.dtype, device=d.device)
+    _check(lib.ldm_space_to_depth2(_ptr(d.contiguous()), batch, h, w, c, _ptr(out), dtype_code(d.dtype), _stream(d)),
+           "ldm_space_to_depth2")
+    return out
+
+
+def posterior_sample(moments, eps):
+    lib = load_library()
+    _gpu(moments, eps)
+    B, C2, H, W = moments.shape
+    z = torch.empty(B, C2 // 2, H, W, dtype=torch.float32, device=moments.device)
+    _check(lib.ldm_posterior_sample(_ptr(moments), _ptr(eps), B, C2 // 2, H * W, _ptr(z), _stream(moments)),
+           "ldm_posterior_sample")
+    return z
+
+
+def posterior_bwd(moments, eps, dz_nhwc):
+    lib = load_library()
+    _gpu(moments, eps, dz_nhwc)
+    B, C2, H, W = moments.shape
+    cs = dz_nhwc.shape[-1]
+    dm = torch.empty_like(moments)
+    _check(lib.ldm_posterior_bwd(_ptr(moments), _ptr(eps), _ptr(dz_nhwc), cs, B, C2 // 2, H * W, _ptr(dm),
+                                 dtype_code(dz_nhwc.dtype), _stream(moments)), "ldm_posterior_bwd")
+    return dm
