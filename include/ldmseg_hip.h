@@ -92,6 +92,8 @@ int ldm_conv2d(const ldm_conv_params* p, ldm_stream_t stream);
  * or bm = 256 for the large-tile bf16 kernel (bn 160); ksplit >= 1 (clamped).  bm = 0
  * restores the built-in heuristic.  Query ldm_conv2d_workspace_bytes after forcing. */
 void ldm_conv2d_force_plan(int bm, int bn, int ksplit);
+/* Tuning hook: LDS ring depth (3 or 4; 0 = planner's choice) of the 128x160 bf16 tile. */
+void ldm_conv2d_force_stages(int stages);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).

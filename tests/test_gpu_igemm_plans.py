@@ -24,14 +24,16 @@ def rel_err(a, b):
 
 @pytest.fixture
 def plan():
-    def set_plan(bm, bn, ks):
+    def set_plan(bm, bn, ks, stages=0):
         K.force_conv_plan(bm, bn, ks)
+        K.force_conv_stages(stages)
     yield set_plan
     K.force_conv_plan(0, 0, 1)
+    K.force_conv_stages(0)
 
 
-PLANS = [(256, 160, 1), (256, 160, 3), (128, 160, 1), (64, 160, 2), (128, 128, 1), (128, 32, 2), (64, 64, 1),
-         (32, 128, 3)]
+PLANS = [(256, 160, 1, 0), (256, 160, 3, 0), (128, 160, 1, 0), (128, 160, 1, 3), (128, 160, 3, 4), (64, 160, 2, 0),
+         (128, 128, 1, 0), (128, 32, 2, 0), (64, 64, 1, 0), (32, 128, 3, 0)]
 SHAPES = [
     # name, B, c0, c1, H, W, Cout, k, stride, upsample
     ("l0", 1, 320, 0, 32, 32, 320, 3, 1, False),
@@ -44,7 +46,7 @@ SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("pl", PLANS, ids=[f"{a}x{b}_k{c}" for a, b, c in PLANS])
+@pytest.mark.parametrize("pl", PLANS, ids=[f"{a}x{b}_k{c}_s{d}" for a, b, c, d in PLANS])
 @pytest.mark.parametrize("case", SHAPES, ids=[s[0] for s in SHAPES])
 def test_conv_plan(case, pl, plan):
     name, B, c0, c1, H, W, Co, k, s, up = case
@@ -67,7 +69,7 @@ def test_conv_plan(case, pl, plan):
     assert rel_err(out.permute(0, 3, 1, 2), ref) < 2e-2
 
 
-@pytest.mark.parametrize("pl", PLANS, ids=[f"{a}x{b}_k{c}" for a, b, c in PLANS])
+@pytest.mark.parametrize("pl", PLANS, ids=[f"{a}x{b}_k{c}_s{d}" for a, b, c, d in PLANS])
 def test_plan_groupnorm_stats(pl, plan):
     """Epilogue GroupNorm partials (two 128-row halves in the large kernel, split-K reduce)."""
     B, H, C, Co, G = 2, 16, 192, 320, 32

@@ -123,7 +123,7 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only", nargs="*")
     ap.add_argument("--plans", nargs="*", default=["auto"],
-                    help="conv tile plans to compare: 'auto' or 'bm,bn,ksplit' (e.g. 256,160,1)")
+                    help="conv tile plans to compare: 'auto' or 'bm,bn,ksplit[,stages]' (e.g. 256,160,1 or 128,160,8,4)")
     a = ap.parse_args()
     names = a.only or list(CASES)
     built = {}
@@ -133,10 +133,12 @@ def main():
             continue
         for pl in a.plans:
             run, fl, nb = CASES[n]()
-            bm, bn, ks = (0, 0, 1) if pl == "auto" else map(int, pl.split(","))
+            f = [0, 0, 1, 0] if pl == "auto" else [int(v) for v in pl.split(",")] + [0]
+            bm, bn, ks, st = f[:4]
 
-            def run_pl(run=run, bm=bm, bn=bn, ks=ks):
+            def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st):
                 K.force_conv_plan(bm, bn, ks)
+                K.force_conv_stages(st)
                 return run()
             built[n if pl == "auto" else f"{n}@{pl}"] = (run_pl, fl, nb)
     for n, (run, _, _) in built.items():

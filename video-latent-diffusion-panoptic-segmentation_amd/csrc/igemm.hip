@@ -555,7 +555,7 @@ __device__ __forceinline__ void write_partial_rows(const ConvArgs& p, float* par
   }
 }
 
-template <typename T, int BM, int BN, bool DMA>
+template <typename T, int BM, int BN, bool DMA, int NS = 2>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   constexpr int ES = sizeof(T);
   constexpr int BK = 128 / ES;  // elements per K tile
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   constexpr int BI = BN / 32;
   constexpr int FM = BM / 32;   // 16x16 fragments per wave along M (wave tile = BM/2)
   constexpr int FN = BN / 32;
-  constexpr int SMEM_MAIN = 2 * (BM + BN) * 8;           // uint4
+  constexpr int SMEM_MAIN = NS * (BM + BN) * 8;          // uint4: NS-stage operand ring
   constexpr int PITCH = BN + 4;                          // staged fp32 row pitch
   // the fp32 tile is staged in two row halves when a whole one would not fit the ring (128x160:
   // keeps the block at 73.7 KB of LDS so two blocks share a CU)
@@ -720,14 +720,37 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
       }
       advance();
     };
-    if (kt0 < kt1) issue_dma(kt0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int kt = kt0; kt < kt1; ++kt) {
-      const int buf = (kt - kt0) & 1;
-      if (kt + 1 < kt1) issue_dma(kt + 1, buf ^ 1);
-      compute(buf);
+    if constexpr (NS == 2) {
+      if (kt0 < kt1) issue_dma(kt0, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const int buf = (kt - kt0) & 1;
+        if (kt + 1 < kt1) issue_dma(kt + 1, buf ^ 1);
+        compute(buf);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    } else {
+      // NS-stage ring (one block per CU: the deep-K split shapes): tiles kt+1 .. kt+NS-2 stay in
+      // flight while tile kt is multiplied; each wave waits only for its own tile kt with a counted
+      // vmcnt (AI + BI LDS-DMA instructions per tile), then one barrier
+      static_assert(NS == 3 || NS == 4, "ring depth");
+      constexpr int PER = AI + BI;
+#pragma unroll
+      for (int i = 0; i < NS - 1; ++i)
+        if (kt0 + i < kt1) issue_dma(kt0 + i, i);
+      int st = 0;
+      for (int kt = kt0; kt < kt1; ++kt) {
+        const int ahead = min(NS - 2, kt1 - 1 - kt);
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kt + NS - 1 < kt1) issue_dma(kt + NS - 1, st == 0 ? NS - 1 : st - 1);
+        compute(st);
+        st = st == NS - 1 ? 0 : st + 1;
+      }
       __syncthreads();
     }
   } else {
@@ -1095,15 +1118,15 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
   }
 }
 
-template <typename T, int BM, int BN>
+template <typename T, int BM, int BN, int NS = 2>
 int launch_bm_bn(ConvArgs a, hipStream_t s) {
   a.tiles_n = (a.n + BN - 1) / BN;
   const int tiles_m = (a.M + BM - 1) / BM;
   a.nblk = tiles_m * a.tiles_n * a.ksplit;
-  if (a.mixed_src)
+  if (NS == 2 && a.mixed_src)
     hipLaunchKernelGGL((igemm_kernel<T, BM, BN, false>), dim3(a.nblk), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL((igemm_kernel<T, BM, BN, true>), dim3(a.nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((igemm_kernel<T, BM, BN, true, NS>), dim3(a.nblk), dim3(256), 0, s, a);
   LDM_CHECK_LAUNCH();
   if (a.ksplit > 1) {
     const int blocks = ((a.M + 63) / 64) * ((a.n + 127) / 128);
@@ -1124,7 +1147,11 @@ int launch_bm(const ConvArgs& a, hipStream_t s, int bn) {
 }
 
 template <typename T>
-int launch_t(const ConvArgs& a, hipStream_t s, int bm, int bn) {
+int launch_t(const ConvArgs& a, hipStream_t s, int bm, int bn, int stages = 2) {
+  if constexpr (sizeof(T) == 2) {
+    if (bm == 128 && bn == 160 && !a.mixed_src && stages == 3) return launch_bm_bn<T, 128, 160, 3>(a, s);
+    if (bm == 128 && bn == 160 && !a.mixed_src && stages == 4) return launch_bm_bn<T, 128, 160, 4>(a, s);
+  }
   if (bm == 32) return launch_bm<T, 32>(a, s, bn);
   if (bm == 64) return launch_bm<T, 64>(a, s, bn);
   return launch_bm<T, 128>(a, s, bn);
@@ -1153,7 +1180,9 @@ inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 struct Plan {
   int bm, bn, ksplit;   // bm == 256: the large-tile bf16 kernel (bn 160)
+  int stages = 2;       // LDS ring depth of the 128x160 kernel (3 / 4: one block per CU)
 };
+int g_force_stages = 0;
 
 // Tuning override (ldm_conv2d_force_plan): applied when it is legal for the call.
 int g_force_bm = 0, g_force_bn = 0, g_force_ks = 0;
@@ -1208,6 +1237,8 @@ Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
   if (es == 2 && waste_ok && split_ok && nk >= 64) {
     pl.bm = 128; pl.bn = 160;
     pl.ksplit = std::max(1, std::min(std::min(8, nk / 16), (512 + t128 / 2) / t128));
+    // <= 256 blocks: one per CU, so a 3-stage ring costs no occupancy (8x8 level: -5 %)
+    if (t128 * pl.ksplit <= 256 && !mixed_src) pl.stages = 3;
     return pl;
   }
   if (big_ok && waste_ok && nk >= 40) {
@@ -1296,6 +1327,8 @@ extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
   g_force_ks = ok ? std::max(1, ksplit) : 0;
 }
 
+extern "C" void ldm_conv2d_force_stages(int stages) { g_force_stages = (stages == 3 || stages == 4) ? stages : 0; }
+
 extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   int es = 0;
   if (validate(q, &es) != LDM_OK) return 0;
@@ -1344,5 +1377,6 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.gn_part = reinterpret_cast<float2*>(q->gn_partial);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (pl.bm == 256) return launch_big(a, s);
-  return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, s, pl.bm, pl.bn) : launch_t<float>(a, s, pl.bm, pl.bn);
+  const int stages = g_force_stages ? g_force_stages : pl.stages;
+  return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, s, pl.bm, pl.bn, stages) : launch_t<float>(a, s, pl.bm, pl.bn);
 }

@@ -60,6 +60,7 @@ EXPORTS = {
     "ldm_conv2d": (_i, [ctypes.POINTER(ConvParams), _vp]),
     "ldm_conv2d_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(ConvParams)]),
     "ldm_conv2d_force_plan": (None, [_i, _i, _i]),
+    "ldm_conv2d_force_stages": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_group_norm_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
     "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _i, _vp]),
@@ -377,6 +378,11 @@ def softmax_rows(s, n, scale, dtype):
 def force_attention_legacy(legacy=True):
     """Tuning hook: route bf16 attention through the 16x16x16-MFMA kernel (A/B only)."""
     load_library().ldm_attention_force_legacy(int(bool(legacy)))
+
+
+def force_conv_stages(stages=0):
+    """Tuning hook: LDS ring depth of the 128x160 tile (3 / 4), 0 = planner."""
+    load_library().ldm_conv2d_force_stages(int(stages))
 
 
 def force_conv_plan(bm=0, bn=0, ksplit=1):
