@@ -114,6 +114,8 @@ int ldm_attention(const ldm_attn_params* p, ldm_stream_t stream);
 /* Tuning hook (benchmarks / tests only): 1 routes bf16 through the 16x16x16-MFMA kernel
  * instead of the 16x16x32 one; 0 restores the default. */
 void ldm_attention_force_legacy(int legacy);
+/* Tuning hook: waves per block of the bf16 flash-attention kernel (4 or 8; 0 = automatic). */
+void ldm_attention_set_waves(int waves);
 /* Training forward: as ldm_attention, and also stores lse[(b * heads + h) * n_q + q] =
  * log2-domain row log-sum-exp of the scaled scores (max2 + log2(l)), consumed by the backward. */
 int ldm_attention_fwd_lse(const ldm_attn_params* p, float* lse, ldm_stream_t stream);

@@ -157,6 +157,22 @@ def test_attention(B, N, L, C, dt):
     assert rel_err(o, ref) < tol(dt)
 
 
+@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("B,N,C", [(2, 4096, 320), (2, 1024, 640), (1, 300, 320), (2, 520, 640)])
+def test_attention_block_waves(B, N, C, waves):
+    """Both block shapes of the bf16 kernel (4 or 8 waves sharing each K/V tile), ragged N."""
+    torch.manual_seed(5)
+    q, k, v = torch.randn(B, N, C), torch.randn(B, N, C), torch.randn(B, N, C)
+    ref = _attn_ref(q, k, v, 8)
+    qkv = torch.cat([q, k, v], -1).to(DEV, torch.bfloat16)
+    K.set_attention_waves(waves)
+    try:
+        o = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, 8, C // 8, N, N, 3 * C, 3 * C, 3 * C)
+    finally:
+        K.set_attention_waves(0)
+    assert rel_err(o, ref) < tol(torch.bfloat16)
+
+
 def test_attention_softmax_spike():
     """Force the online-softmax rescale: a huge logit in the LAST kv tile of some rows."""
     torch.manual_seed(4)

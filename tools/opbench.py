@@ -40,11 +40,12 @@ def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, ge
     return run, flops, None
 
 
-def attn_case(B, N, C, heads=8, legacy=False):
+def attn_case(B, N, C, heads=8, legacy=False, waves=0):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
     def run():
         K.force_attention_legacy(legacy)
+        K.set_attention_waves(waves)
         return K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, C // heads, N, N, 3 * C, 3 * C, 3 * C)
     return run, 4.0 * B * heads * N * N * (C // heads), None
 
@@ -107,6 +108,9 @@ CASES = {
     "attn_1024_d80_legacy": lambda: attn_case(8, 1024, 640, legacy=True),
     "attn_256_d160_legacy": lambda: attn_case(8, 256, 1280, legacy=True),
     "attn_1024_d80": lambda: attn_case(8, 1024, 640),
+    "attn_4096_d40_w8": lambda: attn_case(8, 4096, 320, waves=8),
+    "attn_1024_d80_w8": lambda: attn_case(8, 1024, 640, waves=8),
+    "attn_4096_d40_w4": lambda: attn_case(8, 4096, 320, waves=4),
     "attn_256_d160": lambda: attn_case(8, 256, 1280),
     "gn_l0_fused": lambda: gn_case(8, 4096, 320, True),
     "gn_l0_unfused": lambda: gn_case(8, 4096, 320, False),

@@ -306,8 +306,8 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, v);
 }
 
-template <int DP, int QSUB, bool ONES>
-__global__ __launch_bounds__(256, 2) void attn32_kernel(const AttnArgs p) {
+template <int DP, int QSUB, bool ONES, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn32_kernel(const AttnArgs p) {
   typedef bf16_t T;
   constexpr int ES = 2, EPC = 8;
   constexpr int ND = DP / 16;           // 16-row O^T fragments (P.V covers DP columns)
@@ -325,7 +325,7 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const AttnArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, g = lane >> 4;
   const int h = blockIdx.y, b = blockIdx.z;
-  const int qbase = blockIdx.x * (64 * QSUB) + wave * 16 * QSUB;
+  const int qbase = blockIdx.x * (16 * QSUB * NW) + wave * 16 * QSUB;
 
   const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
   const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const AttnArgs p) {
   auto issue_tile = [&](int kv0, int buf) {
     const unsigned kb = lds0 + (unsigned)(buf * 2 * TILE * ES);
     const unsigned vb = kb + TILE * ES;
-    for (int i = wave; i < RCH; i += 4) {
+    for (int i = wave; i < RCH; i += NW) {
       const int L = i * 64 + lane;
       const int row = L / RCH, c = L - row * RCH;
       const int kv = kv0 + row, d = c * EPC;
@@ -494,10 +494,19 @@ __global__ __launch_bounds__(256, 2) void attn32_kernel(const AttnArgs p) {
   }
 }
 
+int g_attn_waves = 0;   // 0: auto (8 when that still gives >= 256 blocks), 4 or 8: forced
+
 template <int DP, int QSUB, bool ONES>
 int launch32_cfg(const AttnArgs& a, int batch, hipStream_t s) {
-  dim3 grid((a.nq + 64 * QSUB - 1) / (64 * QSUB), a.heads, batch);
-  hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES>), grid, dim3(256), 0, s, a);
+  const int blocks8 = (a.nq + 128 * QSUB - 1) / (128 * QSUB) * a.heads * batch;
+  if (g_attn_waves == 8 || (g_attn_waves == 0 && blocks8 >= 256)) {
+    // 8 waves share every K/V tile (one 512-thread block per CU): half the LDS-DMA bytes per FLOP
+    dim3 grid((a.nq + 128 * QSUB - 1) / (128 * QSUB), a.heads, batch);
+    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 8>), grid, dim3(512), 0, s, a);
+  } else {
+    dim3 grid((a.nq + 64 * QSUB - 1) / (64 * QSUB), a.heads, batch);
+    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES>), grid, dim3(256), 0, s, a);
+  }
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
@@ -904,6 +913,8 @@ extern "C" int ldm_attention(const ldm_attn_params* q, ldm_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   return q->dtype == LDM_BF16 ? launch_bf16(a, q->batch, s) : launch_t<float>(a, q->batch, s);
 }
+
+extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 || waves == 8) ? waves : 0; }
 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
 

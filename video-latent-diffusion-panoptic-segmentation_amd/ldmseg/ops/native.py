@@ -76,6 +76,7 @@ EXPORTS = {
     "ldm_gaussian_posterior": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
     "ldm_attention_fwd_lse": (_i, [ctypes.POINTER(AttnParams), _vp, _vp]),
     "ldm_attention_force_legacy": (None, [_i]),
+    "ldm_attention_set_waves": (None, [_i]),
     "ldm_attention_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_bwd": (_i, [ctypes.POINTER(AttnParams), _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
     "ldm_group_norm_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
@@ -373,6 +374,12 @@ def softmax_rows(s, n, scale, dtype):
     _check(lib.ldm_softmax_rows(_ptr(s), rows, int(n), stride, float(scale), _ptr(p), dtype_code(dtype), _stream(s)),
            "ldm_softmax_rows")
     return p
+
+
+def set_attention_waves(waves=0):
+    """Tuning hook: 4 or 8 waves per flash-attention block (8: every K/V tile serves twice the
+    queries); 0 = automatic (8 when that still gives >= 256 blocks)."""
+    load_library().ldm_attention_set_waves(int(waves))
 
 
 def force_attention_legacy(legacy=True):
