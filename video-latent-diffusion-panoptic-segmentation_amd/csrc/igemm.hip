@@ -746,7 +746,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
         if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
         else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        // raw barrier: __syncthreads()' fence would emit vmcnt(0) and drain the tiles in flight
+        asm volatile("s_barrier" ::: "memory");
         if (kt + NS - 1 < kt1) issue_dma(kt + NS - 1, st == 0 ? NS - 1 : st - 1);
         compute(st);
         st = st == NS - 1 ? 0 : st + 1;
