@@ -128,7 +128,10 @@ def main():
     ap.add_argument("--only", nargs="*")
     ap.add_argument("--plans", nargs="*", default=["auto"],
                     help="conv tile plans to compare: 'auto' or 'bm,bn,ksplit[,stages]' (e.g. 256,160,1 or 128,160,8,4)")
+    ap.add_argument("--lib", default=None, help="load this library build instead (e.g. exp/libabl1.so)")
     a = ap.parse_args()
+    if a.lib:
+        K.load_library(os.path.abspath(a.lib))
     names = a.only or list(CASES)
     built = {}
     for n in names:

@@ -152,7 +152,11 @@ __global__ __launch_bounds__(256, 2) void attn_kernel(const AttnArgs p) {
         float pv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+#if ATTN_ABL == 1   // ablation: no transcendental
+          pv[r] = fmaf(sacc[js][s][r], c2, mneg);
+#else
           pv[r] = __builtin_amdgcn_exp2f(fmaf(sacc[js][s][r], c2, mneg));
+#endif
           if (!ONES) lsum += pv[r];
         }
         if constexpr (ES == 2) {
@@ -300,11 +304,30 @@ __device__ __forceinline__ float max_over_groups(float v) {
   return fmaxf(__uint_as_float(b[0]), __uint_as_float(b[1]));
 }
 
+// IEEE maximum (NaN-propagating) needs no operand canonicalisation and folds to v_maximum3_f32
+// on gfx950; inline asm would hide the MFMA-result read hazard from the compiler
+__device__ __forceinline__ float vmax3(float a, float b, float c) {
+  return __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
+}
+
+__device__ __forceinline__ float max_over_groups_raw(float v) {
+  unsigned u = __float_as_uint(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+  v = vmax3(__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[1]));
+  u = __float_as_uint(v);
+  const auto b = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  return vmax3(__uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[1]));
+}
+
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
   const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
   return __builtin_bit_cast(uint32_t, v);
 }
+
+#ifndef ATTN_ABL
+#define ATTN_ABL 0   // ablation builds only (tools/attn_ablate.sh): 1 no exp2, 2 no QK MFMA, 3 no PV MFMA
+#endif
 
 template <int DP, int QSUB, bool ONES, int NW = 4>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void attn32_kernel(const AttnArgs p) {
@@ -389,7 +412,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn32_kernel(const AttnArgs 
         Frag8<T> ka;
         ka.v = *reinterpret_cast<const uint4*>(krow + 32 * c + 8 * g);
 #pragma unroll
-        for (int s = 0; s < QSUB; ++s) mma_k32(sacc[js][s], ka, q32[s][c]);
+        for (int s = 0; s < QSUB; ++s) {
+#if ATTN_ABL == 2   // ablation: no Q.K^T MFMA
+          sacc[js][s][c & 3] += __uint_as_float(ka.v.x ^ q32[s][c].v.y);
+#else
+          mma_k32(sacc[js][s], ka, q32[s][c]);
+#endif
+        }
       }
     }
     uint2 pk[4][QSUB];                      // bf16 P^T, (kv 4g .. 4g+3 of fragment js) per lane
@@ -402,14 +431,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn32_kernel(const AttnArgs 
           for (int r = 0; r < 4; ++r)
             if (kv0 + 16 * js + 4 * g + r >= p.nkv) sacc[js][s][r] = -INFINITY;
       }
-      float m0 = fmaxf(fmaxf(sacc[0][s][0], sacc[0][s][1]), sacc[0][s][2]);
-      float m1 = fmaxf(fmaxf(sacc[0][s][3], sacc[1][s][0]), sacc[1][s][1]);
-      float m2 = fmaxf(fmaxf(sacc[1][s][2], sacc[1][s][3]), sacc[2][s][0]);
-      float m3 = fmaxf(fmaxf(sacc[2][s][1], sacc[2][s][2]), sacc[2][s][3]);
-      float m4 = fmaxf(fmaxf(sacc[3][s][0], sacc[3][s][1]), sacc[3][s][2]);
-      float mx = fmaxf(fmaxf(m0, m1), m2);
-      mx = fmaxf(fmaxf(mx, m3), m4);
-      mx = max_over_groups(fmaxf(mx, sacc[3][s][3]));
+      // maximum3 straight on the MFMA results (fmaxf would canonicalise every operand first)
+      float m0 = vmax3(sacc[0][s][0], sacc[0][s][1], sacc[0][s][2]);
+      float m1 = vmax3(sacc[0][s][3], sacc[1][s][0], sacc[1][s][1]);
+      float m2 = vmax3(sacc[1][s][2], sacc[1][s][3], sacc[2][s][0]);
+      float m3 = vmax3(sacc[2][s][1], sacc[2][s][2], sacc[2][s][3]);
+      float m4 = vmax3(sacc[3][s][0], sacc[3][s][1], sacc[3][s][2]);
+      float mx = vmax3(m0, m1, m2);
+      mx = vmax3(mx, m3, m4);
+      mx = max_over_groups_raw(vmax3(mx, sacc[3][s][3], sacc[3][s][3]));
       const float ms = mx * c2;
       if (__any(ms > mrun[s] + kRescaleThr)) {
         const float mnew = fmaxf(mrun[s], ms);
@@ -426,7 +456,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn32_kernel(const AttnArgs 
         float pv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+#if ATTN_ABL == 1   // ablation: no transcendental
+          pv[r] = fmaf(sacc[js][s][r], c2, mneg);
+#else
           pv[r] = __builtin_amdgcn_exp2f(fmaf(sacc[js][s][r], c2, mneg));
+#endif
           if (!ONES) lsum += pv[r];
         }
         pk[js][s] = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
@@ -449,25 +483,30 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn32_kernel(const AttnArgs 
         for (int s = 0; s < QSUB; ++s) {
           Frag8<T> pb;
           pb.v = make_uint4(pk[2 * t][s].x, pk[2 * t][s].y, pk[2 * t + 1][s].x, pk[2 * t + 1][s].y);
+#if ATTN_ABL == 3   // ablation: no P.V MFMA
+          oacc[dd][s][t] += __uint_as_float(va.v.x ^ pb.v.y ^ va.v.z ^ pb.v.w);
+#else
           mma_k32(oacc[dd][s], va, pb);
+#endif
         }
       }
     }
   };
 
+  // full tiles in the loop (one compute body: no per-tile copies of the accumulators between
+  // a masked and an unmasked instance), the ragged last tile after it
   const int ntiles = (p.nkv + KVT - 1) / KVT;
+  const int nfull = p.nkv / KVT;
   issue_tile(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < ntiles) issue_tile((t + 1) * KVT, buf ^ 1);
-    const int kv0 = t * KVT;
-    if (kv0 + KVT > p.nkv) compute(buf, kv0, true);
-    else compute(buf, kv0, false);
+  for (int t = 0; t < nfull; ++t) {
+    if (t + 1 < ntiles) issue_tile((t + 1) * KVT, (t + 1) & 1);
+    compute(t & 1, t * KVT, false);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  if (nfull < ntiles) compute(nfull & 1, nfull * KVT, true);
 
   T* op = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * p.d;
 #pragma unroll
