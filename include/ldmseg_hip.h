@@ -94,6 +94,8 @@ int ldm_conv2d(const ldm_conv_params* p, ldm_stream_t stream);
 void ldm_conv2d_force_plan(int bm, int bn, int ksplit);
 /* Tuning hook: LDS ring depth (3 or 4; 0 = planner's choice) of the 128x160 bf16 tile. */
 void ldm_conv2d_force_stages(int stages);
+/* Tuning hook: M panels per tile-raster group of ldm_conv2d (default 8; 1 = row-major tiles). */
+void ldm_conv2d_set_raster_group(int group_m);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).

@@ -128,6 +128,7 @@ def main():
     ap.add_argument("--only", nargs="*")
     ap.add_argument("--plans", nargs="*", default=["auto"],
                     help="conv tile plans to compare: 'auto' or 'bm,bn,ksplit[,stages]' (e.g. 256,160,1 or 128,160,8,4)")
+    ap.add_argument("--groups", nargs="*", type=int, default=[8], help="conv tile-raster groups to compare")
     ap.add_argument("--lib", default=None, help="load this library build instead (e.g. exp/libabl1.so)")
     a = ap.parse_args()
     if a.lib:
@@ -139,15 +140,18 @@ def main():
             built[n] = CASES[n]()
             continue
         for pl in a.plans:
-            run, fl, nb = CASES[n]()
-            f = [0, 0, 1, 0] if pl == "auto" else [int(v) for v in pl.split(",")] + [0]
-            bm, bn, ks, st = f[:4]
+            for gm in a.groups:
+                run, fl, nb = CASES[n]()
+                f = [0, 0, 1, 0] if pl == "auto" else [int(v) for v in pl.split(",")] + [0]
+                bm, bn, ks, st = f[:4]
 
-            def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st):
-                K.force_conv_plan(bm, bn, ks)
-                K.force_conv_stages(st)
-                return run()
-            built[n if pl == "auto" else f"{n}@{pl}"] = (run_pl, fl, nb)
+                def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm):
+                    K.force_conv_plan(bm, bn, ks)
+                    K.force_conv_stages(st)
+                    K.set_conv_raster_group(gm)
+                    return run()
+                name = n if pl == "auto" else f"{n}@{pl}"
+                built[name if len(a.groups) == 1 else f"{name}/g{gm}"] = (run_pl, fl, nb)
     for n, (run, _, _) in built.items():
         run()
     torch.cuda.synchronize()

@@ -347,8 +347,21 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn32_kernel(const AttnArgs 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 15, g = lane >> 4;
-  const int h = blockIdx.y, b = blockIdx.z;
-  const int qbase = blockIdx.x * (16 * QSUB * NW) + wave * 16 * QSUB;
+  // 1-D grid, XCD-aware: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of
+  // (batch, head, q-block) ids and the q-blocks of one head read its K/V from one L2 (with the
+  // 3-D grid the 8 q-blocks of a head landed on 8 XCDs: 8x the K/V misses)
+  int qb, h, b;
+  {
+    const int nqb = (p.nq + 16 * QSUB * NW - 1) / (16 * QSUB * NW);
+    const int bid = blockIdx.x, nblk = gridDim.x;
+    const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
+    const int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    qb = t % nqb;
+    const int hb = t / nqb;
+    h = hb % p.heads;
+    b = hb / p.heads;
+  }
+  const int qbase = qb * (16 * QSUB * NW) + wave * 16 * QSUB;
 
   const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
   const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
@@ -540,11 +553,11 @@ int launch32_cfg(const AttnArgs& a, int batch, hipStream_t s) {
   const int blocks8 = (a.nq + 128 * QSUB - 1) / (128 * QSUB) * a.heads * batch;
   if (g_attn_waves == 8 || (g_attn_waves == 0 && blocks8 >= 256)) {
     // 8 waves share every K/V tile (one 512-thread block per CU): half the LDS-DMA bytes per FLOP
-    dim3 grid((a.nq + 128 * QSUB - 1) / (128 * QSUB), a.heads, batch);
-    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 8>), grid, dim3(512), 0, s, a);
+    const int nblk = (a.nq + 128 * QSUB - 1) / (128 * QSUB) * a.heads * batch;
+    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 8>), dim3(nblk), dim3(512), 0, s, a);
   } else {
-    dim3 grid((a.nq + 64 * QSUB - 1) / (64 * QSUB), a.heads, batch);
-    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES>), grid, dim3(256), 0, s, a);
+    const int nblk = (a.nq + 64 * QSUB - 1) / (64 * QSUB) * a.heads * batch;
+    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES>), dim3(nblk), dim3(256), 0, s, a);
   }
   LDM_CHECK_LAUNCH();
   return LDM_OK;

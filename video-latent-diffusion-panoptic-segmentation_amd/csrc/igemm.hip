@@ -49,12 +49,26 @@ struct ConvArgs {
   float* partial;
   float2* gn_part;    // optional [M/64][n] (sum, sumsq) of the final output values
   int tap_inner;      // K tiles visited channel-block-major, taps inner (see k_state)
+  int group_m;        // M panels per raster group (grouped_tile); 1 = plain row-major tiles
 };
 
 constexpr int kBufFlags = 0x00020000;
 constexpr int kOOB = 0x7ffffff0;  // offset past every num_records: the load returns zeros
 
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+
+// Grouped raster: tile ids run over groups of 8 M panels with the N tiles outer inside a
+// group, so the ~64 tiles an XCD has in flight at once (its contiguous run of ids, see the
+// kernels) share 8 A panels and a few B column tiles from that XCD's L2 instead of streaming
+// all of B once per M panel (GEGLU 640: L2 misses 283 -> ~60 MB per launch).
+__device__ __forceinline__ void grouped_tile(int tile, int tiles_m, int tiles_n, int G, int& tm, int& tn) {
+  const int span = G * tiles_n;
+  const int grp = tile / span, idx = tile - grp * span;
+  const int rows = min(G, tiles_m - grp * G);
+  tm = grp * G + idx % rows;
+  tn = idx / rows;
+}
 
 // Order in which a block visits its K tiles.  Packed K is tap-major (ky, kx, c), but when
 // every tile lies inside one tap (cin % BK == 0) the tiles are visited channel-block-major
@@ -584,7 +598,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   }
   const int split = tile % p.ksplit;
   tile /= p.ksplit;
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  int tm, tn;
+  grouped_tile(tile, (p.M + BM - 1) / BM, p.tiles_n, p.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk_all = p.kpad / BK;
   const int kt0 = (int)((int64_t)nk_all * split / p.ksplit);
@@ -942,7 +957,8 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
   }
   const int split = tile % p.ksplit;
   tile /= p.ksplit;
-  const int tm = tile / p.tiles_n, tn = tile - tm * p.tiles_n;
+  int tm, tn;
+  grouped_tile(tile, (p.M + BM - 1) / BM, p.tiles_n, p.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk_all = p.kpad / BK;
   const int kt0 = (int)((int64_t)nk_all * split / p.ksplit);
@@ -1328,6 +1344,8 @@ extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
   g_force_ks = ok ? std::max(1, ksplit) : 0;
 }
 
+int g_group_m = 8;
+extern "C" void ldm_conv2d_set_raster_group(int g) { g_group_m = g >= 1 ? g : 8; }
 extern "C" void ldm_conv2d_force_stages(int stages) { g_force_stages = (stages == 3 || stages == 4) ? stages : 0; }
 
 extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
@@ -1372,6 +1390,7 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.tiles_n = 0;
   a.nblk = 0;
   a.mixed_src = mixed ? 1 : 0;
+  a.group_m = g_group_m;
   a.tap_inner = (!mixed && q->ksize > 1 && cin % bk == 0 && q->c0 % bk == 0) ? 1 : 0;
   a.ksplit = pl.ksplit;
   a.partial = static_cast<float*>(q->workspace);

@@ -61,6 +61,7 @@ EXPORTS = {
     "ldm_conv2d_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(ConvParams)]),
     "ldm_conv2d_force_plan": (None, [_i, _i, _i]),
     "ldm_conv2d_force_stages": (None, [_i]),
+    "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_group_norm_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
     "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _i, _vp]),
@@ -390,6 +391,11 @@ def force_attention_legacy(legacy=True):
 def force_conv_stages(stages=0):
     """Tuning hook: LDS ring depth of the 128x160 tile (3 / 4), 0 = planner."""
     load_library().ldm_conv2d_force_stages(int(stages))
+
+
+def set_conv_raster_group(group_m=8):
+    """Tuning hook: M panels per tile-raster group (1 = row-major tile order)."""
+    load_library().ldm_conv2d_set_raster_group(int(group_m))
 
 
 def force_conv_plan(bm=0, bn=0, ksplit=1):
