@@ -87,6 +87,7 @@ CASES = {
     "gemm_proj_320": lambda: conv_case(8, 64, 64, 320, 320, k=1, residual=True),
     "gemm_qkv_320": lambda: conv_case(8, 64, 64, 320, 960, k=1),
     "gemm_geglu_320": lambda: conv_case(8, 64, 64, 320, 2560, k=1, geglu=True),
+    "gemm_plain_2560_320": lambda: conv_case(8, 64, 64, 320, 2560, k=1),
     "gemm_ff2_1280": lambda: conv_case(8, 64, 64, 1280, 320, k=1, residual=True),
     "gemm_geglu_1280": lambda: conv_case(8, 16, 16, 1280, 10240, k=1, geglu=True),
     "gemm_qkv_640": lambda: conv_case(8, 32, 32, 640, 1920, k=1),

@@ -50,6 +50,9 @@ __device__ __forceinline__ float erf_fast(float x) {
   return copysignf(fmaf(-y, e, 1.0f), x);
 }
 __device__ __forceinline__ float gelu_f(float x) {  // exact-form (erf) GELU, torch approximate='none'
+#ifdef LDM_ABLATE_GELU   // ablation builds only (tools/ablate.sh)
+  return x;
+#endif
   return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f));
 }
 

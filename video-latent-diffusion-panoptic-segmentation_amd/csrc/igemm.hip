@@ -1135,12 +1135,14 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
   }
 }
 
+int g_force_stages = 0;   // tuning hook: 1 register-staged operands, 3 / 4 ring depth, 0 planner
+
 template <typename T, int BM, int BN, int NS = 2>
 int launch_bm_bn(ConvArgs a, hipStream_t s) {
   a.tiles_n = (a.n + BN - 1) / BN;
   const int tiles_m = (a.M + BM - 1) / BM;
   a.nblk = tiles_m * a.tiles_n * a.ksplit;
-  if (NS == 2 && a.mixed_src)
+  if (NS == 2 && (a.mixed_src || g_force_stages == 1))
     hipLaunchKernelGGL((igemm_kernel<T, BM, BN, false>), dim3(a.nblk), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((igemm_kernel<T, BM, BN, true, NS>), dim3(a.nblk), dim3(256), 0, s, a);
@@ -1199,7 +1201,6 @@ struct Plan {
   int bm, bn, ksplit;   // bm == 256: the large-tile bf16 kernel (bn 160)
   int stages = 2;       // LDS ring depth of the 128x160 kernel (3 / 4: one block per CU)
 };
-int g_force_stages = 0;
 
 // Tuning override (ldm_conv2d_force_plan): applied when it is legal for the call.
 int g_force_bm = 0, g_force_bn = 0, g_force_ks = 0;
@@ -1346,7 +1347,9 @@ extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
 
 int g_group_m = 8;
 extern "C" void ldm_conv2d_set_raster_group(int g) { g_group_m = g >= 1 ? g : 8; }
-extern "C" void ldm_conv2d_force_stages(int stages) { g_force_stages = (stages == 3 || stages == 4) ? stages : 0; }
+extern "C" void ldm_conv2d_force_stages(int stages) {
+  g_force_stages = (stages == 1 || stages == 3 || stages == 4) ? stages : 0;   // 1: register-staged operands
+}
 
 extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   int es = 0;
