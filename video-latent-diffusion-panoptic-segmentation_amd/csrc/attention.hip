@@ -329,8 +329,8 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
 #define ATTN_ABL 0   // ablation builds only (tools/attn_ablate.sh): 1 no exp2, 2 no QK MFMA, 3 no PV MFMA
 #endif
 
-template <int DP, int QSUB, bool ONES, int NW = 4>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void attn32_kernel(const AttnArgs p) {
+template <int DP, int QSUB, bool ONES, int NW = 4, int OCC = 8 / NW>
+__global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) {
   typedef bf16_t T;
   constexpr int ES = 2, EPC = 8;
   constexpr int ND = DP / 16;           // 16-row O^T fragments (P.V covers DP columns)
@@ -563,11 +563,26 @@ int launch32_cfg(const AttnArgs& a, int batch, hipStream_t s) {
   return LDM_OK;
 }
 
+template <int DP, int QSUB, bool ONES, int NW, int OCC>
+int launch_occ(const AttnArgs& a, int batch, hipStream_t s) {
+  const int nblk = (a.nq + 16 * QSUB * NW - 1) / (16 * QSUB * NW) * a.heads * batch;
+  hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, NW, OCC>), dim3(nblk), dim3(64 * NW), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
 template <int DP>
 int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
   // query subtiles per wave: as many as stay spill-free (the ONES variant has no l registers)
   constexpr int QS1 = DP <= 48 ? 4 : (DP <= 96 ? 2 : 1);
   constexpr int QS0 = DP <= 96 ? 2 : 1;
+  if constexpr (DP == 48) {
+    // head_dim 40 (the 64x64 level): 8 waves x 2 query subtiles at 118 VGPRs -> two blocks per
+    // CU whose phases drift apart, so one block's softmax VALU runs beside the other's MFMAs
+    // (N=4096: 295 -> 265 us against one 8-wave block of 4 subtiles); needs >= 2 blocks per CU
+    const int nblk2 = (a.nq + 255) / 256 * a.heads * batch;
+    if (a.d == DP - 8 && g_attn_waves == 0 && nblk2 >= 512) return launch_occ<DP, 2, true, 8, 2>(a, batch, s);
+  }
   if (a.d == DP - 8) return launch32_cfg<DP, QS1, true>(a, batch, s);
   return launch32_cfg<DP, QS0, false>(a, batch, s);
 }
