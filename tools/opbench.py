@@ -104,6 +104,11 @@ CASES = {
     "gemm_geglu_1280_l2": lambda: conv_case(8, 16, 16, 1280, 10240, k=1, geglu=True),
     "conv3_l3_2560": lambda: conv_case(8, 8, 8, 2560, 1280, c1=1280, residual=True, stats=True),
     "conv3_s2_l2": lambda: conv_case(8, 16, 16, 1280, 1280, stride=2, stats=True),
+    "conv3_s2_l0": lambda: conv_case(8, 64, 64, 320, 320, stride=2, stats=True),
+    "conv3_s2_l1": lambda: conv_case(8, 32, 32, 640, 640, stride=2, stats=True),
+    "conv3_l1_in_320": lambda: conv_case(8, 32, 32, 320, 640, temb=True, stats=True),
+    "conv3_l1_res_640": lambda: conv_case(8, 32, 32, 640, 640, residual=True, stats=True),
+    "conv3_l2_in_640": lambda: conv_case(8, 16, 16, 640, 1280, temb=True, stats=True),
     "attn_4096_d40": lambda: attn_case(8, 4096, 320),
     "attn_4096_d40_legacy": lambda: attn_case(8, 4096, 320, legacy=True),
     "attn_1024_d80_legacy": lambda: attn_case(8, 1024, 640, legacy=True),

@@ -714,6 +714,9 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;   // LDS byte address of smem
     const int wv = __builtin_amdgcn_readfirstlane(wave);
     auto issue_dma = [&](int kt, int buf) {
+#ifdef LDM_ABL_NO_LOADS   // ablation build: operands never fetched (LDS holds stale data)
+      return;
+#endif
       const unsigned abase = lds0 + (unsigned)(buf * (BM + BN) * 8 * 16);
       const unsigned bbase = abase + BM * 8 * 16;
       const int ch = ks_.ch;
@@ -818,6 +821,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     }
   }
 
+#ifdef LDM_ABL_NO_EPILOGUE   // ablation build (tools/ablate.sh): accumulators kept alive, no epilogue
+  {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (t == 12345.f) reinterpret_cast<float*>(p.out)[tid] = t;
+    return;
+  }
+#endif
   // ------------------------------------------------------------------ fused epilogue
   // phase 1: raw accumulators -> LDS [EPI_ROWS][PITCH] fp32 (per row half when EPI_H == 2:
   // wave row wm owns rows [wm * BM/2, (wm+1) * BM/2) = half wm)
@@ -1235,6 +1249,9 @@ Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
   const int tiles_big = ((M + 255) / 256) * tn_big;
   pl.ksplit = 1;
   if (q->out_layout == LDM_OUT_GEGLU) {
+    // deep K with >= 512 128x160 tiles: two blocks per CU beat the one-block 256x160 kernel
+    // (GEGLU 1280 -> 10240 at 16x16, B=8: 88 -> 78 us)
+    if (es == 2 && waste_ok && nk >= 20 && tiles_of(128, 160) >= 512) { pl.bm = 128; pl.bn = 160; return pl; }
     if (big_ok && waste_ok && nk >= 20 && tiles_big >= 240) { pl.bm = 256; pl.bn = 160; return pl; }
     pl.bm = M <= 32 ? 32 : (M <= 64 ? 64 : 128);
     pl.bn = 128;
@@ -1246,6 +1263,11 @@ Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
   // at the UNet shapes, profiles/r01c_*)
   const int t128 = tiles_of(128, 160), t64 = tiles_of(64, 160);
   if (es == 2 && waste_ok && t128 >= 512) { pl.bm = 128; pl.bn = 160; return pl; }
+  // wide N, moderate K, one wave of 128x128 tiles (QKV 1280 -> 3840 at 16x16: 43 -> 32 us vs 64x160)
+  if (es == 2 && q->n >= 2048 && nk >= 20 && nk < 64 && tiles_of(128, 128) >= 400) {
+    pl.bm = 128; pl.bn = 128;
+    return pl;
+  }
   if (es == 2 && waste_ok && t64 >= 400 && nk <= 128 && (tiles_big < 240 || nk < 40)) {
     pl.bm = 64; pl.bn = 160;
     return pl;
@@ -1266,6 +1288,13 @@ Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
       pl.ksplit = std::min((256 + tiles_big - 1) / tiles_big, std::min(4, nk / 32));
       return pl;
     }
+  }
+  // moderate K over 192-400 64x160 tiles (the 64x64 -> 32x32 Downsample2D conv, 320 ch): split K to
+  // ~512 blocks instead of 64x64 tiles (39 -> 35 us)
+  if (es == 2 && waste_ok && split_ok && nk >= 32 && t64 >= 192 && t64 < 400) {
+    pl.bm = 64; pl.bn = 160;
+    pl.ksplit = std::max(1, std::min(nk / 16, (512 + t64 - 1) / t64));
+    return pl;
   }
   const int bn_small = q->n <= 32 ? 32 : (q->n <= 64 ? 64 : 128);
   if (M <= 64) {                     // a handful of rows (time-embedding MLP)
