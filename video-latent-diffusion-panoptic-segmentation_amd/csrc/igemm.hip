@@ -821,6 +821,40 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     }
   }
 
+  // GEGLU straight from the accumulators: with the 16-column hidden/gate interleave of the packed
+  // weight, fragments j (hidden) and j + 1 (gate) of a wave hold the two halves of the same 4
+  // output channels of the same pixel in the same lane, so h * gelu(g) needs no LDS staging and
+  // no barrier — the staged epilogue was ~40 % of a K=320 GEGLU launch (tile ablations).
+  // Each lane stores 8 B per (fragment pair, row); the 4 pairs of a 64-channel output row segment
+  // are written by consecutive instructions of the same wave and merge in L2.
+  if constexpr (sizeof(T) == 2 && FN % 2 == 0 && (BN / 2) % 32 == 0) {
+    if (p.out_layout == LDM_OUT_GEGLU && p.ksplit == 1 && !p.out_f32 &&
+        (reinterpret_cast<uintptr_t>(p.out) & 7) == 0) {
+      const int NO = p.n >> 1;
+#pragma unroll
+      for (int j = 0; j < FN; j += 2) {
+        const int pc = n0 + wn * (BN / 2) + j * 16 + 4 * g;   // packed column of the hidden values
+        if (pc >= p.n) continue;
+        const int oc = (pc >> 5) * 16 + (pc & 15);            // output channel
+        float bh[4], bg[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          bh[r] = p.bias ? p.bias[pc + r] : 0.f;
+          bg[r] = p.bias ? p.bias[pc + 16 + r] : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int m = m0 + wm * (BM / 2) + i * 16 + lr;
+          if (m >= p.M) continue;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = (acc[i][j][r] + bh[r]) * gelu_f(acc[i][j + 1][r] + bg[r]);
+          store4<T>(p.out, (int64_t)m * NO + oc, v, false);
+        }
+      }
+      return;
+    }
+  }
 #ifdef LDM_ABL_NO_EPILOGUE   // ablation build (tools/ablate.sh): accumulators kept alive, no epilogue
   {
     float t = 0.f;
