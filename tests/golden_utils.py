@@ -52,3 +52,33 @@ DDIM_CONFIGS = {
     "sigmoid_x0": dict(beta_schedule="sigmoid", beta_start=0.0001, beta_end=0.02,
                        prediction_type="sample", weight="fixed", clip_sample=False),
 }
+
+
+# ------------------------------------------------------------------ loop-level fixtures
+# (tests/golden/make_golden_loops.py): a reduced-width UNet built by this package's module tree
+# with seeded torch default init, non-trivial norm affines / biases, and this package's
+# modify_encoder (pinned separately against the reference's at 320 channels).  The fixture
+# stores state_hash() of the weights it ran with, so a drift in construction order fails loudly.
+LOOP_UNET = dict(block_out_channels=(64, 128, 128, 128), cross_attention_dim=None)
+
+
+def build_loop_unet(UNet, cond=4, seed=0):
+    torch.manual_seed(seed)
+    u = UNet(**LOOP_UNET)
+    with torch.no_grad():
+        for _, p in u.named_parameters():
+            if p.ndim == 1:
+                p.add_(torch.randn_like(p) * 0.1)
+    u.modify_encoder(in_channels=8, init_mode_seg="copy", init_mode_image="random", cond_channels=cond,
+                     init_mode_cond="random")
+    u.freeze_layers(["time_embedding"])
+    return u
+
+
+def state_hash(module):
+    import hashlib
+    h = hashlib.sha256()
+    for k, v in sorted(module.state_dict().items()):
+        h.update(k.encode())
+        h.update(v.detach().float().cpu().contiguous().numpy().tobytes())
+    return h.hexdigest()

@@ -1,6 +1,7 @@
 """encode_inputs / decode_latents (trainers_ldm_cond.py:336-444) on the HIP path against the
 same composition of torch F.interpolate and the golden-pinned seg-VAE oracle (oracle/vae.py),
 and the RGB path through GeneralVAEImage against oracle/autoencoder_kl.py (unpinned)."""
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -8,7 +9,7 @@ import torch.nn.functional as F
 from golden_utils import VAE_CONFIGS
 from ldmseg.models import GeneralVAESeg
 from ldmseg.models.autoencoder_kl import GeneralVAEImage
-from ldmseg.pipelines.latents import decode_latents, encode_inputs
+from ldmseg.pipelines.latents import color_map, decode_latents, encode_inputs
 from oracle import autoencoder_kl as oae
 from oracle import vae as ovae
 
@@ -46,10 +47,15 @@ def test_decode_latents_logits_and_predictions():
     logits = decode_latents(v.to(DEV), z.to(DEV), return_logits=True)
     ref = ovae.decode(sd, z * (1.0 / v.scaling_factor), VAE_CONFIGS["kitti"])
     assert rel(logits, ref) < 1e-4
-    pred = decode_latents(v, z.to(DEV), threshold_output=True, mask_th=0.5, ignore_label=255).cpu()
+    pred = decode_latents(v, z.to(DEV), threshold_output=True, mask_th=0.5, ignore_label=255,
+                          return_predictions=True).cpu()
     exp = logits.cpu().argmax(1)
     exp[torch.softmax(logits.cpu(), 1).max(1)[0] < 0.5] = 255
     assert torch.equal(pred, exp)
+    # the reference's return value (:437-438): encode_seg colour map of the predictions, uint8 NHWC
+    img = decode_latents(v, z.to(DEV), threshold_output=True, mask_th=0.5, ignore_label=255)
+    assert isinstance(img, np.ndarray) and img.dtype == np.uint8 and img.shape == (*exp.shape, 3)
+    assert np.array_equal(img, color_map()[exp.numpy().astype(np.uint8)])
 
 
 def test_encode_inputs_rgb_path():

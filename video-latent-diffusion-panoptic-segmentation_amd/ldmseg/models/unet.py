@@ -14,8 +14,10 @@ stay checkpoint-compatible, trainers_ldm_cond.py:1846-1848,1891-1894); the arith
   Down/Up     stride-2 conv / conv reading the input through a nearest-2x upsample
   out         GN+SiLU -> conv_out written straight to NCHW
 
-Only the inference forward is native this round (training backward is
-the next row); gradients do not flow through it.
+In train mode with grad enabled, ``forward`` goes through ``_UNetTrainFn``: the same HIP
+forward keeping its activations, and the hand-written HIP backward of models/unet_train.py
+(gradients flow to every trainable parameter, as under torch autograd; not to the input
+sample, which the reference's training never needs).
 """
 import json
 import math

@@ -232,7 +232,9 @@ class UNetTrainGraph:
         b1, e1 = (self.G.get(x1) if x1 is not None else (None, False))
         K.group_norm_bwd(x0, B, H * W, r.groups, s["mr1"], *p["n1"], K.ACT_SILU, dh1, x1=x1, add_src=add, dx0=b0,
                          dx1=b1, acc0=e0, acc1=e1, dgamma=dg1, dbeta=db1, acc_params=acc1)
-        self.on_ready([q for q in r.parameters() if q.requires_grad])
+        # time_emb_proj's gradient is written by _temb_bwd after the whole graph: report it there
+        temb = {id(q) for q in r.time_emb_proj.parameters()}
+        self.on_ready([q for q in r.parameters() if q.requires_grad and id(q) not in temb])
 
     def _dtemb_slice(self, off, n):
         return self.dtemb_parts.setdefault(off, torch.empty(self.B, n, dtype=torch.float32, device=self.dev))

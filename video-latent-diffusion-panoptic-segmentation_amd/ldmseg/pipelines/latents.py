@@ -8,6 +8,7 @@ either the logits or the argmax / confidence-thresholded predictions (ldm_panopt
 The RGB latents come from GeneralVAEImage.encode, the segmentation latents from
 GeneralVAESeg.encode — the same encode_func contract as the reference.
 """
+import numpy as np
 import torch
 
 from ..ops import native as K
@@ -36,14 +37,50 @@ def encode_inputs(images, encode_func, scaling_factor, latent_size, resize=(192,
     return latents, (latents.clone() if not sample_posterior else means)
 
 
+def color_map(N=256, normalized=False):
+    """The PASCAL colour map of ldmseg/utils/utils.py:240-258 (bit i of the label goes to bit
+    7 - i//3 of channel i % 3)."""
+    ids = np.arange(N)
+    cmap = np.zeros((N, 3), dtype=np.int64)
+    c = ids.copy()
+    for j in range(8):
+        for ch in range(3):
+            cmap[:, ch] |= ((c >> ch) & 1) << (7 - j)
+        c = c >> 3
+    return cmap.astype(np.float32) / 255 if normalized else cmap.astype(np.uint8)
+
+
+_CMAP = {}
+
+
+def encode_seg(predictions):
+    """TrainerDiffusion.encode_seg (trainers_ldm_cond.py:326-334): int label maps [B, H, W]
+    -> colour images uint8 [B, H, W, 3] (labels taken mod 256, as ``astype(np.uint8)``).  The
+    table lookup runs on the predictions' device; the result is a host numpy array, as the
+    reference returns."""
+    dev = predictions.device
+    if dev not in _CMAP:
+        _CMAP[dev] = torch.from_numpy(color_map()).to(dev)
+    return _CMAP[dev][(predictions & 255).long()].cpu().numpy()
+
+
 @torch.no_grad()
 def decode_latents(vae_semseg, latents, return_logits=False, threshold_output=False, mask_th=0.5, ignore_label=255,
-                   weight_dtype=torch.float32):
-    """-> logits fp32 [B, K, H, W] (return_logits) or int64 predictions [B, H, W] (the input of
-    the reference's encode_seg colour map, :433-437)."""
+                   weight_dtype=torch.float32, return_predictions=False):
+    """decode_latents (trainers_ldm_cond.py:398-444).  return_logits: fp32 logits [B, K, H, W]
+    (GPU).  Otherwise the reference's output: argmax (+ ignore_label where the max softmax
+    probability < mask_th when threshold_output) colour-mapped to uint8 numpy [B, H, W, 3]; a
+    3-channel decoder gives the (x/2 + 0.5) uint8 image.  return_predictions=True (an opt-in
+    this build adds) returns the int64 label map [B, H, W] on the GPU instead of its colours."""
     z = K.resize_bilinear(latents.float(), size=tuple(latents.shape[-2:]), mul=1.0 / vae_semseg.scaling_factor,
                           out_dtype=weight_dtype)
     images = vae_semseg.decode(z).float()
     if return_logits:
         return images
-    return threshold_predictions(images, mask_th, ignore_label, threshold_output)
+    if images.shape[1] == 3:
+        img = (images / 2 + 0.5).clamp(0, 1)
+        return (img.cpu().permute(0, 2, 3, 1).numpy() * 255).astype(np.uint8)
+    pred = threshold_predictions(images, mask_th, ignore_label, threshold_output)
+    if return_predictions:
+        return pred
+    return encode_seg(pred)

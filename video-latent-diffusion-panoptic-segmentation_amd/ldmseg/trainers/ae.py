@@ -23,6 +23,7 @@ coordinates, posterior noise) come from torch's generator; ``rand`` / ``randn`` 
 (the parity test feeds the reference's own draws).
 """
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from ..models.vae import LayerNorm2d
@@ -277,7 +278,6 @@ class PointLosses:
         cls_t = torch.tensor(cls, dtype=torch.int32, device=logits.device)
         planes = img_t * C + cls_t
         num_masks = float(len(cls))
-        import torch.distributed as dist
         if dist.is_available() and dist.is_initialized():
             t = torch.tensor([num_masks], device=logits.device)
             dist.all_reduce(t)
@@ -316,6 +316,10 @@ class AETrainStep:
         self.exp_avg_sq = torch.zeros_like(self.flat.data)
         self.sqsum = torch.zeros((), dtype=torch.float64, device=self.flat.data.device)
         self.step_count = 0
+        # DDP (main_worker_ae.py:80-89): rank 0's weights at construction, averaged gradients
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        if self.world > 1:
+            dist.broadcast(self.flat.data, 0)
 
     def _sink(self, p):
         return self.flat.view_of(p, self.flat.grad), False
@@ -340,6 +344,9 @@ class AETrainStep:
         if self.w["ce"] != 1.0 or self.w["mask"] != 1.0:
             raise NotImplementedError("loss weights other than 1 (base.yaml) are not wired into the gradient")
         graph.backward(dlog)
+        if self.world > 1:
+            dist.all_reduce(self.flat.grad)
+            self.flat.grad.mul_(1.0 / self.world)
         self.step_count += 1
         K.sq_norm(self.flat.grad, out=self.sqsum)
         K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.segs, 1, self.step_count,

@@ -92,20 +92,37 @@ class LDMTrainStep:
         lr_factor_func = lr_factor_func or unet.get_lr_func
         self.base_lr = lr
         self.seg_hp = []
+        # get_optim_unet's grouping key (optim.py:196-243): the construction-time lr, plus the
+        # weight decay only for norm layers — other parameters carry no per-group weight_decay,
+        # so a norm group stays separate even when weight_decay_norm == weight_decay
+        self.seg_key = []
         for p, o in zip(self.flat.params, self.flat.offsets):
             plr = lr * lr_factor_func(names[id(p)])
             wd = weight_decay_norm if id(p) in norm_ids else weight_decay
             self.seg_hp.append([o, o + p.numel(), plr, wd])
+            self.seg_key.append((plr, wd if id(p) in norm_ids else None))
         self._upload_segments()
         self.exp_avg = torch.zeros_like(self.flat.data)
         self.exp_avg_sq = torch.zeros_like(self.flat.data)
         self.step_count = 0
+        # DistributedDataParallel(...) broadcasts rank 0's parameters when it is constructed
+        # (tools/main_ldm.py:184-197): every rank starts from the same weights even when their
+        # init seeds differ or a checkpoint was loaded on rank 0 only.
+        self._broadcast(self.flat.data)
         self.sqsum = torch.zeros((), dtype=torch.float64, device=dev)
         self.gen = None
         if seed is not None:
             self.gen = torch.Generator(device=dev)
             self.gen.manual_seed(seed)
         unet.invalidate_packed()
+
+    def _src(self):
+        return dist.get_global_rank(self.group, 0) if self.group is not None else 0
+
+    def _broadcast(self, *tensors):
+        if self.world > 1:
+            for t in tensors:
+                dist.broadcast(t, self._src(), group=self.group)
 
     def _upload_segments(self):
         recs = b"".join(struct.pack("<qqff", s, e, lr, wd) for s, e, lr, wd in self.seg_hp)
@@ -129,8 +146,9 @@ class LDMTrainStep:
                 if not q.requires_grad or id(q) in memo or id(q) not in self.flat.index:
                     continue
                 memo.add(id(q))
-                _, _, lr, wd = self.seg_hp[self.flat.index[id(q)]]
-                groups.setdefault((lr, wd), []).append(q)
+                # grouped by the construction-time key, not the scheduled lr: after set_lr every
+                # group has the same lr, but the reference optimizer keeps its groups
+                groups.setdefault(self.seg_key[self.flat.index[id(q)]], []).append(q)
         return list(groups.items())
 
     def _group_defaults(self, lr, wd):
@@ -142,7 +160,8 @@ class LDMTrainStep:
     def state_dict(self):
         """torch.optim.AdamW.state_dict() of the same optimizer (fp32 moments, ``step``)."""
         state, pgs, idx = {}, [], 0
-        for (lr, wd), ps in self.reference_param_groups():
+        for _, ps in self.reference_param_groups():
+            _, _, lr, wd = self.seg_hp[self.flat.index[id(ps[0])]]        # the group's current lr
             ids = []
             for q in ps:
                 if self.step_count > 0:
@@ -181,6 +200,25 @@ class LDMTrainStep:
             raise ValueError("per-parameter step counts differ; the fused AdamW keeps one count")
         self.step_count = steps.pop() if steps else 0
         self._upload_segments()
+        if self.world > 1:
+            # collective: every rank resumes (trainers_ldm_cond.py:1879-1914 runs on all ranks);
+            # rank 0's moments, step count and learning rates win, like its parameters at init
+            cnt = torch.tensor([float(self.step_count)], dtype=torch.float64, device=self.flat.data.device)
+            self._broadcast(self.exp_avg, self.exp_avg_sq, cnt, self.segs)
+            self.step_count = int(cnt.item())
+            self._download_segments()
+
+    def _download_segments(self):
+        import numpy as np
+        rec = np.frombuffer(self.segs.cpu().numpy().tobytes(), dtype=np.dtype([("s", "<i8"), ("e", "<i8"),
+                                                                                ("lr", "<f4"), ("wd", "<f4")]))
+        for seg, r in zip(self.seg_hp, rec):
+            seg[2], seg[3] = float(r["lr"]), float(r["wd"])
+
+    def broadcast_parameters(self):
+        """Re-sync every rank's weights to rank 0's (collective), e.g. after a load on rank 0."""
+        self._broadcast(self.flat.data)
+        self.unet.invalidate_packed()
 
     def _sink(self, p):
         return self.flat.view_of(p, self.flat.grad), False
