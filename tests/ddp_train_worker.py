@@ -35,6 +35,7 @@ def main():
     st = LDMTrainStep(u, sched, lr=1e-3, weight_decay=0.05, clip_grad=1.0, self_condition=True,
                       compute_dtype=torch.float32, bucket_mb=1)
     init = st.flat.data.detach().cpu().clone()
+    frozen = torch.cat([q.detach().reshape(-1).float().cpu() for q in u.parameters() if not q.requires_grad])
     n = d["latents"].shape[1] // world
     sl = slice(rank * n, (rank + 1) * n)
     losses = []
@@ -42,7 +43,7 @@ def main():
         g = lambda k: d[k][i, sl].to(dev)        # noqa: E731
         losses.append(st.train_step(g("latents"), g("rgb"), g("mask"), timesteps=g("t"), noise=g("noise")).item())
     torch.cuda.synchronize()
-    torch.save({"init": init, "final": st.flat.data.detach().cpu(), "losses": torch.tensor(losses),
+    torch.save({"init": init, "frozen": frozen, "final": st.flat.data.detach().cpu(), "losses": torch.tensor(losses),
                 "buckets": len(st.bucketer.buckets)}, f"{out_prefix}{rank}.pt")
     dist.barrier()
     dist.destroy_process_group()

@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from golden_utils import VAE_CONFIGS, build_loop_unet, load, vae_state_dict
-from ldmseg.evaluations.dvpq import dvpq_summary, write_dvpq_frame
+from ldmseg.evaluations.dvpq import dvpq_summary, panoptic_to_dvpq, write_dvpq_frame
 from ldmseg.models import GeneralVAESeg, UNet
 from ldmseg.models.autoencoder_kl import GeneralVAEImage
 from ldmseg.pipelines.sample import sample_panoptic
@@ -70,13 +70,11 @@ def _oracle_chain(ae, u, vs, rgb):
         return opan.postprocess(logits, (H, W), torch.ones(B, H, W, dtype=torch.bool), [(H, W)] * B, **HEAD)
 
 
-def _panoptic_pngs(d, cleaned_frames, tag):
-    """Class-agnostic segments (compute_pq's category_id 1 for every segment) as category 0,
-    instance = segment id; dropped pixels are void (255)."""
+def _panoptic_pngs(d, cleaned_frames, tag, gt=False):
+    """Predictions through panoptic_to_dvpq (segments -> category 0, dropped -> 19); the ground
+    truth's dropped pixels are void (255)."""
     for f, c in enumerate(cleaned_frames):
-        c = np.asarray(c)
-        cat = np.where(c >= 0, 0, 255)
-        ins = np.where(c >= 0, c + 1, 0)
+        cat, ins = panoptic_to_dvpq(c, dropped_category=255 if gt else 19)
         write_dvpq_frame(os.path.join(d, tag), f"000000_{f:06d}_", cat, ins)
 
 
@@ -89,6 +87,16 @@ def _read_clip(d, tag):
     ids = [np.array(Image.open(os.path.join(d, tag, c))).astype(np.int32) * MAX_INS +
            np.array(Image.open(os.path.join(d, tag, i))).astype(np.int32) for c, i in zip(cats, inss)]
     return np.concatenate(ids, axis=1)
+
+
+def _ground_truth(r, seed):
+    g2 = r.copy()
+    g2[np.random.default_rng(seed).random(r.shape) < 0.1] = -1
+    vals, cnt = np.unique(r[r >= 0], return_counts=True)
+    order = vals[np.argsort(cnt)]
+    g2[r == order[-1]] = -1
+    g2[r == order[1]] = order[0]
+    return g2
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -109,21 +117,15 @@ def test_sample_panoptic_matches_oracle_chain_and_dvpq(graph, tmp_path):
         ids, info = res[f]["panoptic_seg"]
         assert sorted(s["id"] for s in info) == sorted((np.unique(ref[f][ref[f] >= 0]) + 1).tolist())
         assert torch.equal(ids.cpu(), torch.from_numpy(mine[f]) + 1)
-    # DVPQ: both outputs as eval_dvpq PNGs, scored against one ground truth (the oracle's own map,
-    # shifted 3 columns, with its largest segment made void)
-    gt = []
-    for r in ref:
-        g2 = np.roll(r, 3, axis=1)
-        vals, cnt = np.unique(g2[g2 >= 0], return_counts=True)
-        g2 = g2.copy()
-        g2[g2 == vals[cnt.argmax()]] = -1
-        gt.append(g2)
+    # DVPQ: both outputs as eval_dvpq PNGs, scored against one ground truth: the oracle's own map
+    # with 10 % of its pixels void, its largest segment void and its two smallest merged
+    gt = [_ground_truth(r, seed=f) for f, r in enumerate(ref)]
     _panoptic_pngs(tmp_path, mine, "pred")
     _panoptic_pngs(tmp_path, ref, "oracle")
-    _panoptic_pngs(tmp_path, gt, "gt")
+    _panoptic_pngs(tmp_path, gt, "gt", gt=True)
     pq = {}
     for tag in ("pred", "oracle"):
         acc = odvpq.vpq_eval(_read_clip(tmp_path, tag), _read_clip(tmp_path, "gt"))
         pq[tag] = dvpq_summary(*acc, num_things=1, num_classes=1)[0]
-    assert pq["oracle"] > 0.0
+    assert 0.0 < pq["oracle"] < 100.0
     assert abs(pq["pred"] - pq["oracle"]) <= 0.1, pq

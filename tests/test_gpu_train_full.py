@@ -136,7 +136,8 @@ def test_ddp_world2_equals_single_process_on_concatenated_batch(tmp_path):
     assert rcs == [0, 0], rcs
     r0, r1 = (torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(2))
     assert r0["buckets"] > 10
-    assert torch.equal(r0["init"], r1["init"])                      # the rank-0 broadcast
+    assert torch.equal(r0["init"], r1["init"])                      # the rank-0 broadcast ...
+    assert torch.equal(r0["frozen"], r1["frozen"])                  # ... of the frozen time_embedding too
     assert torch.equal(r0["final"], r1["final"])                    # one averaged update on both ranks
     # single process, same initial weights (rank 0's seed), whole batch per iteration
     u = build_loop_unet(UNet, cond=4, seed=10).to(DEV)
@@ -146,7 +147,10 @@ def test_ddp_world2_equals_single_process_on_concatenated_batch(tmp_path):
     for i in range(I):
         loss = st.train_step(d["latents"][i].to(DEV), d["rgb"][i].to(DEV), d["mask"][i].to(DEV),
                              timesteps=d["t"][i].to(DEV), noise=d["noise"][i].to(DEV)).item()
-        assert abs(loss - 0.5 * (r0["losses"][i] + r1["losses"][i]).item()) / loss < 1e-4
+        # step 0 runs on identical weights; step 1 after one AdamW update, whose normalised step
+        # turns ~1e-6 gradient differences of near-zero gradients into O(lr) weight differences
+        tol = 1e-6 if i == 0 else 1e-3
+        assert abs(loss - 0.5 * (r0["losses"][i] + r1["losses"][i]).item()) / loss < tol, i
     single = st.flat.data.cpu()
     worst = []
     for p in st.flat.params:

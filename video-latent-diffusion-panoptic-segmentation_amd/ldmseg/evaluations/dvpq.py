@@ -34,6 +34,18 @@ def write_dvpq_frame(pan_dir, stem, cat, ins):
     ins_img.save(os.path.join(pan_dir, f"{stem}ins.png"))
 
 
+def panoptic_to_dvpq(cleaned, category=0, dropped_category=19):
+    """compute_pq's class-agnostic output (cleaned_pred: segment label >= 0, -1 = dropped,
+    trainers_ldm_cond.py:1302-1326, every segment ``category_id`` 1) -> the (cat, ins) pair of a
+    DVPQ prediction: kept pixels get ``category`` and instance = label + 1 (its panoptic id);
+    dropped pixels get ``dropped_category`` with instance 0 — 19, the category eval_dvpq.py
+    itself gives predictions it discards (:143), since a predicted category 255 would index past
+    its 20 per-class accumulators (:98-99)."""
+    c = cleaned.cpu().numpy() if torch.is_tensor(cleaned) else np.asarray(cleaned)
+    keep = c >= 0
+    return np.where(keep, category, dropped_category), np.where(keep, c + 1, 0)
+
+
 def reduce_pq_accumulators(iou, tp, fn, fp, group=None):
     """Sum the per-class accumulators over all ranks (float64; returns four numpy arrays).
     Uses the process group's device: CUDA tensors for nccl (RCCL), host tensors for gloo."""
@@ -55,4 +67,5 @@ def dvpq_summary(iou, tp, fn, fp, num_things=8, num_classes=19, eps=1e-10):
     sq = iou / (tp + eps)
     rq = tp / (tp + 0.5 * fn + 0.5 * fp + eps)
     pq = sq * rq
-    return pq.mean() * 100, pq[:num_things].mean() * 100, pq[num_things:].mean() * 100
+    mean = lambda a: a.mean() * 100 if a.size else float("nan")     # noqa: E731
+    return mean(pq), mean(pq[:num_things]), mean(pq[num_things:])

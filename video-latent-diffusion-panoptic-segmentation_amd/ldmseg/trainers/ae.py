@@ -320,6 +320,8 @@ class AETrainStep:
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         if self.world > 1:
             dist.broadcast(self.flat.data, 0)
+            for t in [q.data for q in vae.parameters() if id(q) not in self.flat.index] + list(vae.buffers()):
+                dist.broadcast(t, 0)
 
     def _sink(self, p):
         return self.flat.view_of(p, self.flat.grad), False

@@ -105,10 +105,11 @@ class LDMTrainStep:
         self.exp_avg = torch.zeros_like(self.flat.data)
         self.exp_avg_sq = torch.zeros_like(self.flat.data)
         self.step_count = 0
-        # DistributedDataParallel(...) broadcasts rank 0's parameters when it is constructed
+        # DistributedDataParallel(...) broadcasts rank 0's module state — every parameter, the
+        # frozen time_embedding included, and every buffer — when it is constructed
         # (tools/main_ldm.py:184-197): every rank starts from the same weights even when their
         # init seeds differ or a checkpoint was loaded on rank 0 only.
-        self._broadcast(self.flat.data)
+        self.broadcast_parameters()
         self.sqsum = torch.zeros((), dtype=torch.float64, device=dev)
         self.gen = None
         if seed is not None:
@@ -216,8 +217,12 @@ class LDMTrainStep:
             seg[2], seg[3] = float(r["lr"]), float(r["wd"])
 
     def broadcast_parameters(self):
-        """Re-sync every rank's weights to rank 0's (collective), e.g. after a load on rank 0."""
-        self._broadcast(self.flat.data)
+        """Re-sync every rank's module state to rank 0's (collective), e.g. after a load on rank 0:
+        the flat trainable buffer in one message, then the frozen parameters and buffers."""
+        if self.world > 1:
+            self._broadcast(self.flat.data)
+            self._broadcast(*[q.data for q in self.unet.parameters() if id(q) not in self.flat.index],
+                            *[b for b in self.unet.buffers()])
         self.unet.invalidate_packed()
 
     def _sink(self, p):
