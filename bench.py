@@ -73,9 +73,18 @@ def roofline(unet, stepper, ts, nsteps, dtype):
             ms = v["ms"] / nsteps
             print(f"{f:10s} {s:44s} {v['launches'] // nsteps:3d} {ms:8.3f} "
                   f"{v['flops'] / nsteps / ms / 1e9:7.1f} {v['bytes'] / nsteps / ms / 1e6:7.1f}", file=sys.stderr)
-    per_step ={k: dict(launches=v["launches"] // nsteps, ms=round(v["ms"] / nsteps, 4),
-                        gflop=round(v["flops"] / nsteps / 1e9, 2), mb=round(v["bytes"] / nsteps / 1e6, 2))
-                for k, v in fam.items()}
+    peak_tf = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_FP32_TFLOPS
+    per_step = {}
+    for k, v in fam.items():
+        e = dict(launches=v["launches"] // nsteps, ms=round(v["ms"] / nsteps, 4),
+                 gflop=round(v["flops"] / nsteps / 1e9, 2), mb=round(v["bytes"] / nsteps / 1e6, 2))
+        sec = v["ms"] * 1e-3
+        if v["flops"] > 0:      # MFMA-bound family: fraction of the dense MFMA peak
+            e["tflops"] = round(v["flops"] / sec / 1e12, 1)
+            e["frac_mfma"] = round(v["flops"] / sec / 1e12 / peak_tf, 4)
+        e["gbs"] = round(v["bytes"] / sec / 1e9, 1)
+        e["frac_hbm"] = round(v["bytes"] / sec / 1e9 / PEAK_HBM_GBS, 4)
+        per_step[k] = e
     dom = max(fam, key=lambda k: fam[k]["ms"])
     d = fam[dom]
     if d["flops"] > 0:
@@ -118,7 +127,8 @@ def cpu_baseline(unet, budget_s=25.0):
     bounded sample: whole frames of the T=8 step until ~budget_s, scaled to steps/s."""
     from oracle import ddim as oddim
     from oracle import unet as ounet
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(os.cpu_count() or 1, 16)
+    host = host_cores()
+    threads = host["usable"]
     torch.set_num_threads(threads)
     sd = {k: v.detach().float().cpu() for k, v in unet.state_dict().items()}
     cfg = dict(unet.config)
@@ -136,8 +146,32 @@ def cpu_baseline(unet, budget_s=25.0):
             frames += 1
     per_step = elapsed / frames * 8
     return {"value": round(1.0 / per_step, 5), "unit": "steps/s", "cores": threads, "kind": "port",
+            "host": host,
             "sample": f"{frames} frame(s) of one T=8 denoising step (UNet fwd + DDIM, fp32, 64x64), "
                       f"{elapsed:.1f} s, scaled x{8 / frames:g} to one 8-frame step"}
+
+
+def host_cores():
+    """The CPU baseline's thread count: os.cpu_count(), capped by what this process
+    may actually run on — its CPU affinity and its cgroup CPU quota (a GPU box shares a large host:
+    os.cpu_count() there counts the whole machine, and oversubscribing a 16-core quota would
+    understate the CPU).  Everything is reported."""
+    n = os.cpu_count() or 1
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else n
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        import psutil
+        phys = psutil.cpu_count(logical=False)
+    except Exception:   # noqa: BLE001
+        phys = None
+    usable = min(n, aff, quota or n)
+    return {"os_cpu_count": n, "affinity": aff, "cgroup_quota_cpus": quota, "physical_cores": phys, "usable": usable}
 
 
 def main():
@@ -151,6 +185,7 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=2)
+    ap.add_argument("--repeats", type=int, default=5, help="timed windows of --steps steps; value from the median")
     ap.add_argument("--mode", default="denoise", choices=["denoise", "train", "sample", "ae"],
                     help="denoise: the headline metric; train: config 3's DDP training iteration; "
                          "sample: config 4's full clip sampling (encode -> 50 DDIM steps -> decode -> panoptic); "
@@ -185,17 +220,21 @@ def main():
 
     for i in range(args.warmup):
         stepper.run(ts[i % len(ts)], last=False)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        stepper.run(ts[k % len(ts)], last=False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     from ldmseg.utils import max_over_ranks
-    elapsed = max_over_ranks(time.perf_counter() - t0, device=dev)
+
+    def window():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            stepper.run(ts[k % len(ts)], last=False)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return max_over_ranks(time.perf_counter() - t0, device=dev)
+    windows = [window() for _ in range(args.repeats)]
+    elapsed = sorted(windows)[len(windows) // 2]          # median window (median of 5)
     finite = bool(torch.isfinite(stepper.lat).all().item())
 
     rl = roofline(unet, stepper, ts, args.profile_steps, dtype) if rank == 0 else None
@@ -215,6 +254,7 @@ def main():
                        "global_batch": B * world, "seq_len": L * L,
                        "parallelism": f"replicas x{world} (independent clips, no data-path collective)"},
             "outputs_finite": finite,
+            "windows_ms_per_step": [round(w / args.steps * 1e3, 3) for w in windows],
             "roofline": rl,
             "cpu_baseline": cpu,
         }
@@ -318,8 +358,46 @@ def main_ae(args):
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
         "data": "synthetic: blobby 20-class KITTI-shaped targets, their 5+5 bit planes; random-init VAE (1.80 M)",
         "config": {"workload": "AE train iteration, B=4 frames 192x640", "global_batch": 4},
-        "loss": round(loss.item(), 5), "reference_cpu_s_per_iter": "0.93-1.31 (8 CPU cores, SURVEY.md §6)"}),
+        "loss": round(loss.item(), 5),
+        "cpu_baseline": None if args.no_cpu_baseline else cpu_baseline_ae(vae, bits, targets)}),
         flush=True)
+
+
+def cpu_baseline_ae(vae, bits, targets, budget_s=20.0):
+    """Config 1 on the host cores: the oracle AE iteration (oracle/ae.py: the reference's VAE
+    forward with posterior sampling + point losses, autograd backward) + clip 3.0 + torch AdamW,
+    fp32, the same B=4 x 10 x 192 x 640 batch; whole iterations until ~budget_s."""
+    from oracle import ae as oae
+    host = host_cores()
+    torch.set_num_threads(host["usable"])
+    sd = {k: v.detach().float().cpu() for k, v in vae.state_dict().items()}
+    cfg = dict(in_channels=10, int_channels=256, out_channels=30, block_out_channels=(32, 64, 128, 256),
+               latent_channels=4, num_latents=2, num_upscalers=2, norm_num_groups=32)
+    b, t = bits.float().cpu(), targets.cpu()
+    g = torch.Generator().manual_seed(0)
+    rand = lambda *shape: torch.rand(*shape, generator=g)          # noqa: E731
+    randn = lambda shape: torch.randn(shape, generator=g)          # noqa: E731
+    params = {k: v.clone() for k, v in sd.items()}
+    opt_state = {}
+    iters, elapsed = 0, 0.0
+    while elapsed < budget_s and iters < 5:
+        t0 = time.perf_counter()
+        _, _, _, grads = oae.train_iteration(params, cfg, b, t, rand, randn)
+        gl = [grads[k] for k in params if grads.get(k) is not None]
+        torch.nn.utils.clip_grad_norm_(gl, 3.0)
+        if not opt_state:
+            ps = [torch.nn.Parameter(params[k]) for k in params]
+            opt_state["opt"] = torch.optim.AdamW(ps, lr=1e-4)
+            opt_state["ps"] = ps
+        for p_, k in zip(opt_state["ps"], params):
+            p_.grad = grads.get(k)
+        opt_state["opt"].step()
+        params = {k: p_.detach() for p_, k in zip(opt_state["ps"], params)}
+        elapsed += time.perf_counter() - t0
+        iters += 1
+    return {"value": round(iters / elapsed, 4), "unit": "iterations/s", "cores": host["usable"], "kind": "port",
+            "host": host, "sample": f"{iters} AE iteration(s) (fwd + point losses + bwd + clip + AdamW, fp32, B=4 "
+                                    f"10x192x640), {elapsed:.1f} s"}
 
 
 TRAIN_METRIC = "LDM training iterations/sec (2 clips x T=8 per GPU, 4x64x64 latents, self-conditioning)"

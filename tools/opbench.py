@@ -40,6 +40,13 @@ def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, ge
     return run, flops, None
 
 
+def mm_case(M, K, N):
+    """torch.mm (hipBLASLt) on the same GEMM shape: the library reference point, no epilogue."""
+    a = torch.randn(M, K, device=DEV).to(BF)
+    b = torch.randn(K, N, device=DEV).to(BF)
+    return (lambda: torch.mm(a, b)), 2.0 * M * K * N, None
+
+
 def attn_case(B, N, C, heads=8, legacy=False, waves=0):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
@@ -109,6 +116,21 @@ CASES = {
     "conv3_l1_in_320": lambda: conv_case(8, 32, 32, 320, 640, temb=True, stats=True),
     "conv3_l1_res_640": lambda: conv_case(8, 32, 32, 640, 640, residual=True, stats=True),
     "conv3_l2_in_640": lambda: conv_case(8, 16, 16, 640, 1280, temb=True, stats=True),
+    "mm_8192": lambda: mm_case(8192, 8192, 8192),
+    "mm_4096": lambda: mm_case(4096, 4096, 4096),
+    "mm_geglu_320": lambda: mm_case(32768, 320, 2560),
+    "mm_qkv_320": lambda: mm_case(32768, 320, 960),
+    "mm_proj_320": lambda: mm_case(32768, 320, 320),
+    "mm_ff2_1280": lambda: mm_case(32768, 1280, 320),
+    "mm_geglu_640": lambda: mm_case(8192, 640, 5120),
+    "mm_proj_640": lambda: mm_case(8192, 640, 640),
+    "mm_ff2_2560": lambda: mm_case(8192, 2560, 640),
+    "mm_geglu_1280": lambda: mm_case(2048, 1280, 10240),
+    "mm_proj_1280": lambda: mm_case(2048, 1280, 1280),
+    "mm_conv_l0_320": lambda: mm_case(32768, 2880, 320),
+    "mm_conv_l1_640": lambda: mm_case(8192, 5760, 640),
+    "mm_conv_l2_1280": lambda: mm_case(2048, 11520, 1280),
+    "mm_conv_l3_1280": lambda: mm_case(512, 11520, 1280),
     "attn_4096_d40": lambda: attn_case(8, 4096, 320),
     "attn_4096_d40_legacy": lambda: attn_case(8, 4096, 320, legacy=True),
     "attn_1024_d80_legacy": lambda: attn_case(8, 1024, 640, legacy=True),
