@@ -53,7 +53,7 @@ enum {
  * W is pre-packed [n_alloc][kpad] (K = ksize*ksize*(c0+c1) padded with zeros to kpad).
  * ------------------------------------------------------------------------------------- */
 enum { LDM_OUT_NHWC = 0, LDM_OUT_NCHW = 1, LDM_OUT_GEGLU = 2, LDM_OUT_SHUFFLE2 = 3 };
-enum { LDM_ACT_NONE = 0, LDM_ACT_SILU = 1 };
+enum { LDM_ACT_NONE = 0, LDM_ACT_SILU = 1, LDM_ACT_RELU = 2, LDM_ACT_SIGMOID = 3 };
 
 typedef struct {
   const void* a0;          /* NHWC [batch][h_in][w_in][c0] */

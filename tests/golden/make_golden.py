@@ -470,11 +470,64 @@ def gen_ae():
     print("ae.npz:", len(out), "arrays", "ce", out["ce"], "mask", out["mask"])
 
 
+# --------------------------------------------------------------------------------------
+# PoseExpNet (config 5's pose network, posenet/posenet.py:21-96)
+# --------------------------------------------------------------------------------------
+POSE_CASES = {
+    # name: (seed, B, H, W, nb_ref_imgs, output_exp, train_mode, init_weights)
+    "kitti_256x512": (1, 2, 256, 512, 2, False, False, False),
+    "exp_train_64x128": (2, 2, 64, 128, 2, True, True, True),
+    "exp_eval_odd_72x100": (3, 1, 72, 100, 2, True, False, False),
+    "one_ref_128x128": (4, 1, 128, 128, 1, False, False, True),
+}
+
+
+def _state_sha(m):
+    import hashlib
+    h = hashlib.sha256()
+    for k, v in sorted(m.state_dict().items()):
+        h.update(k.encode())
+        h.update(v.detach().float().contiguous().numpy().tobytes())
+    return h.hexdigest()
+
+
+def gen_posenet():
+    """The reference PoseExpNet, torch default init (or its init_weights: xavier_uniform) under
+    torch.manual_seed(seed); inputs U(0,1) frames from a seeded generator.  The weights are not
+    stored: the test rebuilds them with the drop-in module under the same seed and checks the
+    state sha256 recorded here."""
+    spec = importlib.util.spec_from_file_location("ref_posenet", os.path.join(REF, "posenet", "posenet.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    out = {}
+    for name, (seed, B, H, W, nref, exp, train, xavier) in POSE_CASES.items():
+        torch.manual_seed(seed)
+        net = mod.PoseExpNet(nb_ref_imgs=nref, output_exp=exp)
+        if xavier:
+            net.init_weights()
+        net.train(train)
+        g = torch.Generator().manual_seed(100 + seed)
+        tgt = torch.rand(B, 3, H, W, generator=g)
+        refs = [torch.rand(B, 3, H, W, generator=g) for _ in range(nref)]
+        with torch.no_grad():
+            r = net(tgt, refs)
+        masks, pose = r
+        out[f"{name}__state_sha"] = np.array(_state_sha(net))
+        out[f"{name}__pose"] = pose.numpy()
+        if train:
+            for i, m in enumerate(masks):
+                if m is not None:
+                    out[f"{name}__mask{i + 1}"] = m.numpy()
+        elif masks is not None:
+            out[f"{name}__mask1"] = masks.numpy()
+        out[f"{name}__cfg"] = np.array([seed, B, H, W, nref, int(exp), int(train), int(xavier)], np.int64)
+    out["names"] = np.array(list(POSE_CASES))
+    np.savez_compressed(os.path.join(HERE, "posenet.npz"), **out)
+    print("posenet.npz:", len(out), "arrays")
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    gen_codec()
-    gen_ddim()
-    gen_vae()
-    gen_vpq()
-    gen_panoptic()
-    gen_ae()
+    which = sys.argv[1:] or ["codec", "ddim", "vae", "vpq", "panoptic", "ae", "posenet"]
+    for w in which:
+        globals()[f"gen_{w}"]()

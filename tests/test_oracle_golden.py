@@ -147,3 +147,32 @@ def test_ae_iteration_oracle():
     for name in z["names"]:
         ref = torch.from_numpy(z[f"g__{name}"])
         assert (grads[str(name)] - ref).norm() <= 1e-4 * ref.norm(), name
+
+
+def test_posenet_oracle_matches_reference_golden():
+    """oracle/posenet.py against the reference PoseExpNet's outputs (posenet.npz), weights rebuilt
+    by the drop-in module under the same seed (state sha256 checked)."""
+    import hashlib
+    from oracle import posenet as opose
+    from posenet.posenet import PoseExpNet
+    z = load("posenet.npz")
+    for name in [str(n) for n in z["names"]]:
+        seed, B, H, W, nref, exp, train, xavier = z[f"{name}__cfg"].tolist()
+        torch.manual_seed(seed)
+        net = PoseExpNet(nb_ref_imgs=nref, output_exp=bool(exp))
+        if xavier:
+            net.init_weights()
+        h = hashlib.sha256()
+        for k, v in sorted(net.state_dict().items()):
+            h.update(k.encode())
+            h.update(v.detach().float().contiguous().numpy().tobytes())
+        assert h.hexdigest() == str(z[f"{name}__state_sha"])
+        g = torch.Generator().manual_seed(100 + seed)
+        tgt = torch.rand(B, 3, H, W, generator=g)
+        refs = [torch.rand(B, 3, H, W, generator=g) for _ in range(nref)]
+        with torch.no_grad():
+            pose, masks = opose.forward(net.state_dict(), tgt, refs, output_exp=bool(exp))
+        np.testing.assert_allclose(pose.numpy(), z[f"{name}__pose"], rtol=1e-5, atol=1e-7)
+        if exp:
+            for i in range(4 if train else 1):
+                np.testing.assert_allclose(masks[i].numpy(), z[f"{name}__mask{i + 1}"], rtol=1e-5, atol=1e-6)

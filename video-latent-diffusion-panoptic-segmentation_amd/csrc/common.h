@@ -36,6 +36,13 @@ template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float v) { return f
 
 // x * sigmoid(x) with v_exp + v_rcp (1 ulp) instead of an IEEE division sequence
 __device__ __forceinline__ float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+// epilogue activation (LDM_ACT_*): SiLU (the UNet), ReLU / sigmoid (PoseExpNet, posenet.py:7-19,76-79)
+__device__ __forceinline__ float act_f(float x, int act) {
+  if (act == LDM_ACT_SILU) return silu_f(x);
+  if (act == LDM_ACT_RELU) return fmaxf(x, 0.f);
+  if (act == LDM_ACT_SIGMOID) return __builtin_amdgcn_rcpf(1.0f + __expf(-x));
+  return x;
+}
 // erf via Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7 absolute): one v_rcp, one v_exp and a
 // degree-5 Horner chain instead of ocml erff's ~40-instruction path.
 __device__ __forceinline__ float erf_fast(float x) {

@@ -171,9 +171,7 @@ __device__ __forceinline__ void finish4(const ConvArgs& p, int b, int pix, int m
   const bool f32o = p.out_f32 != 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    float x = v[r] + bias4[r] + temb4[r];
-    if (p.act == LDM_ACT_SILU) x = silu_f(x);
-    v[r] = x;
+    v[r] = act_f(v[r] + bias4[r] + temb4[r], p.act);
   }
   if (p.out_layout == LDM_OUT_NCHW) {
 #pragma unroll
@@ -497,9 +495,9 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
           v[0] += ta.x; v[1] += ta.y; v[2] += ta.z; v[3] += ta.w;
           v[4] += tb.x; v[5] += tb.y; v[6] += tb.z; v[7] += tb.w;
         }
-        if (p.act == LDM_ACT_SILU) {
+        if (p.act != LDM_ACT_NONE) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = silu_f(v[k]);
+          for (int k = 0; k < 8; ++k) v[k] = act_f(v[k], p.act);
         }
         if (res) {
           float rr[8];
@@ -1359,7 +1357,8 @@ int validate(const ldm_conv_params* q, int* es_out) {
   if (q->dtype != LDM_F32 && q->dtype != LDM_BF16) return LDM_ERR_ARG;
   const int es = q->dtype == LDM_F32 ? 4 : 2;
   const int ce = 16 / es;
-  if (q->ksize != 1 && q->ksize != 3) return LDM_ERR_ARG;
+  if (q->ksize != 1 && q->ksize != 3 && q->ksize != 5 && q->ksize != 7) return LDM_ERR_ARG;
+  if (q->act < LDM_ACT_NONE || q->act > LDM_ACT_SIGMOID) return LDM_ERR_ARG;
   if (q->stride != 1 && q->stride != 2) return LDM_ERR_ARG;
   if (q->upsample < 0 || q->upsample > 2 || (q->upsample && (q->stride != 1))) return LDM_ERR_ARG;
   if (q->batch <= 0 || q->h_in <= 0 || q->w_in <= 0 || q->h_out <= 0 || q->w_out <= 0) return LDM_ERR_ARG;

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(PKG_ROOT, "lib", "libldmseg_hip.so")
 
 F32, BF16 = 0, 1
 OUT_NHWC, OUT_NCHW, OUT_GEGLU, OUT_SHUFFLE2 = 0, 1, 2, 3
-ACT_NONE, ACT_SILU = 0, 1
+ACT_NONE, ACT_SILU, ACT_RELU, ACT_SIGMOID = 0, 1, 2, 3
 PRED = {"epsilon": 0, "sample": 1, "v_prediction": 2}
 POST_ACT = {"none": 0, "tanh": 1, "sigmoid": 2, "clip": 3}
 
@@ -230,9 +230,28 @@ class PackedConv:
     GEGLU projection in 16-column blocks; ``shuffle2`` packs a ConvTranspose2d(k=2, s=2).
     """
 
-    def __init__(self, weight, bias, dtype, cin_pad=None, geglu=False, shuffle2=False):
+    def __init__(self, weight, bias, dtype, cin_pad=None, geglu=False, shuffle2=False, convt4=False):
         w = weight.detach()
-        if shuffle2:                       # ConvTranspose2d weight [cin, cout, 2, 2]
+        if convt4:
+            # ConvTranspose2d(k=4, s=2, p=1) weight [cin, cout, 4, 4] as a 3x3 conv (pad 1) with
+            # 4 * cout outputs, one per output phase (dy, dx), + the pixel-shuffle epilogue:
+            # out[2y+dy, 2x+dx] = sum over taps (ty, tx) of in[y-1+ty, x-1+tx] . W[:, :, ky, kx]
+            # with ky = 3 + dy - 2 ty (valid 0..3), kx likewise
+            cin, cout = w.shape[0], w.shape[1]
+            cp = cin_pad or cin
+            w3 = torch.zeros(2, 2, cout, 3, 3, cp, dtype=w.dtype, device=w.device)
+            for dy in range(2):
+                for dx in range(2):
+                    for ty in range(3):
+                        for tx in range(3):
+                            ky, kx = 3 + dy - 2 * ty, 3 + dx - 2 * tx
+                            if 0 <= ky <= 3 and 0 <= kx <= 3:
+                                w3[dy, dx, :, ty, tx, :cin] = w[:, :, ky, kx].t()
+            wp = w3.reshape(4 * cout, 9 * cp)
+            b = None if bias is None else bias.detach().float().repeat(4)
+            self.ksize, self.cin, self.n = 3, cp, 4 * cout
+            self.cin_real = cin
+        elif shuffle2:                     # ConvTranspose2d weight [cin, cout, 2, 2]
             cin, cout = w.shape[0], w.shape[1]
             wp = w.permute(2, 3, 1, 0).reshape(4 * cout, cin)          # n = (dy*2+dx)*cout + co
             b = None if bias is None else bias.detach().float().repeat(4)
@@ -242,7 +261,7 @@ class PackedConv:
             if w.ndim == 2:
                 w = w[:, :, None, None]
             cout, cin, kh, kw = w.shape
-            assert kh == kw and kh in (1, 3), "only 1x1 / 3x3 kernels are on the path"
+            assert kh == kw and kh in (1, 3, 5, 7), "1x1 / 3x3 / 5x5 / 7x7 kernels"
             cp = cin_pad or cin
             self.cin_real = cin
             if cp != cin:
@@ -266,7 +285,7 @@ class PackedConv:
         self.bias = None if b is None else b.contiguous()
         self.dtype = dtype
         self.geglu = geglu
-        self.shuffle2 = shuffle2
+        self.shuffle2 = shuffle2 or convt4
 
 
 def packed_rows(t, bias=None):
@@ -307,14 +326,15 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
         _contig(t, nm)
     if x0.dtype != pc.dtype or (x1 is not None and x1.dtype != pc.dtype):
         raise TypeError(f"conv input dtype {x0.dtype} != packed weight dtype {pc.dtype}")
-    if pc.ksize == 1:
+    k = pc.ksize
+    if k == 1:
         ho, wo = h, w
     elif upsample:
         ho, wo = 2 * h, 2 * w
     elif pad_mode == 1:                    # diffusers Downsample2D(padding=0): F.pad (0, 1, 0, 1)
         ho, wo = (h + 1 - 3) // stride + 1, (w + 1 - 3) // stride + 1
-    else:
-        ho, wo = (h + 2 - 3) // stride + 1, (w + 2 - 3) // stride + 1
+    else:                                  # padding (k - 1) // 2
+        ho, wo = (h + k - 1 - k) // stride + 1, (w + k - 1 - k) // stride + 1
     n = pc.n
     if out_layout == OUT_GEGLU:
         shape = (batch, ho, wo, n // 2)
