@@ -96,6 +96,9 @@ void ldm_conv2d_force_plan(int bm, int bn, int ksplit);
 void ldm_conv2d_force_stages(int stages);
 /* Tuning hook: M panels per tile-raster group of ldm_conv2d (default 8; 1 = row-major tiles). */
 void ldm_conv2d_set_raster_group(int group_m);
+/* Tuning hook: the halo-tiled 3x3 kernel (bf16, stride 1, 64-channel-aligned sources, output
+ * width 64 or 32): 0 = planner's choice, 1 = never, 2 = whenever legal. */
+void ldm_conv2d_set_halo(int mode);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).
@@ -113,6 +116,11 @@ typedef struct {
 } ldm_attn_params;
 
 int ldm_attention(const ldm_attn_params* p, ldm_stream_t stream);
+/* BASELINE config 5 ("fp8 MFMA attention", pose-conditioned video LDM at T=16): as ldm_attention
+ * (bf16 only), with the P.V product on the e4m3 MFMA — P and V rounded to OCP e4m3, fp32
+ * accumulation; Q.K^T and the softmax in bf16 / fp32.  Accuracy mode: on gfx950 the non-scaled
+ * fp8 MFMA issues at the bf16 rate. */
+int ldm_attention_fp8(const ldm_attn_params* p, ldm_stream_t stream);
 /* Tuning hook (benchmarks / tests only): 1 routes bf16 through the 16x16x16-MFMA kernel
  * instead of the 16x16x32 one; 0 restores the default. */
 void ldm_attention_force_legacy(int legacy);

@@ -1,0 +1,88 @@
+"""BASELINE config 5 shapes on the HIP path: T=16 frames of 256x512 KITTI frames -> 32x64
+latents (non-square: N = 2048 tokens at the 64-channel... 320-channel level, 512 / 128 / 32
+below), the full SD-1.4 UNet (cross-attention removed, 8-channel conv_in).  Frames are
+independent, so the oracle (oracle/unet.py, fp32 CPU) checks the first and the
+last frame of the 16-frame batch, with per-frame timesteps.  fp32 1e-3 (north-star bar), bf16
+5e-2."""
+import pytest
+import torch
+
+from ldmseg.models import UNet
+from ldmseg.ops import native as K
+from oracle import unet as ounet
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def _sd14():
+    torch.manual_seed(0)
+    with torch.device(DEV):
+        u = UNet()
+    u.remove_cross_attention()
+    u.modify_encoder(in_channels=8, init_mode_seg="copy", init_mode_image="zero")
+    return u.eval()
+
+
+def test_unet_sd14_t16_32x64_matches_oracle():
+    u = _sd14()
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(16, 8, 32, 64, generator=g)
+    t = torch.randint(0, 1000, (16,), generator=g)
+    out = u(x.to(DEV), t.to(DEV)).sample
+    assert out.shape == (16, 4, 32, 64)
+    sd = {k: v.detach().cpu() for k, v in u.state_dict().items()}
+    torch.set_num_threads(16)
+    with torch.no_grad():
+        ref = ounet.forward(sd, dict(u.config), x[[0, 15]], t[[0, 15]])
+    assert rel(out[[0, 15]], ref) < 1e-3
+    ub = u.to(torch.bfloat16)
+    outb = ub(x.to(DEV, torch.bfloat16), t.to(DEV)).sample
+    assert rel(outb[[0, 15]], ref) < 5e-2
+
+
+@pytest.mark.parametrize("N,C", [(2048, 320), (4096, 320), (512, 640), (128, 1280), (100, 320)])
+def test_fp8_attention_within_stated_tolerance(N, C):
+    """ldm_attention_fp8 (P.V on e4m3) against torch fp32 attention on the same bf16 inputs.
+    Bar: relative L2 error <= 5e-2 and max-abs error <= 1.5e-1 of the output's max-abs.  e4m3
+    keeps 3 mantissa bits (relative rounding <= 2^-4, RMS ~3.6 % for uniform mantissas); with a
+    flat softmax the output is a mean of V and its rounding errors shrink with the output itself,
+    so the relative error stays at the e4m3 level (measured 3.7e-2 at N=2048, bf16 2.1e-3)."""
+    heads, B = 8, 2
+    d = C // heads
+    g = torch.Generator(device=DEV).manual_seed(N + C)
+    qkv = (torch.randn(B, N, 3 * C, device=DEV, generator=g) * 1.5).to(torch.bfloat16)
+    out = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, d, N, N, 3 * C, 3 * C, 3 * C, fp8=True)
+    x = qkv.float().view(B, N, 3, heads, d).permute(2, 0, 3, 1, 4)
+    ref = torch.softmax(x[0] @ x[1].transpose(-1, -2) * d ** -0.5, -1) @ x[2]
+    ref = ref.permute(0, 2, 1, 3).reshape(B, N, C)
+    l2 = ((out.float() - ref).norm() / ref.norm()).item()
+    mx = ((out.float() - ref).abs().max() / ref.abs().max()).item()
+    bf = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, d, N, N, 3 * C, 3 * C, 3 * C)
+    l2_bf16 = ((bf.float() - ref).norm() / ref.norm()).item()
+    print(f"N={N} C={C}: fp8 rel-L2 {l2:.3e} max {mx:.3e}; bf16 rel-L2 {l2_bf16:.3e}")
+    assert l2 <= 5e-2 and mx <= 1.5e-1
+
+
+def test_unet_config5_fp8_attention_close_to_oracle():
+    """The config-5 UNet at T=16, 32x64 latents with fp8 P.V in every self-attention: frames 0
+    and 15 against the fp32 oracle, bar 1.2e-1 (bf16 compute + e4m3 P.V, see the op test)."""
+    u = _sd14()
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(16, 8, 32, 64, generator=g)
+    t = torch.full((16,), 500, dtype=torch.long)
+    sd = {k: v.detach().cpu() for k, v in u.state_dict().items()}
+    torch.set_num_threads(16)
+    with torch.no_grad():
+        ref = ounet.forward(sd, dict(u.config), x[[0, 15]], t[[0, 15]])
+    ub = u.to(torch.bfloat16)
+    ub.set_attention_fp8(True)
+    out = ub(x.to(DEV, torch.bfloat16), t.to(DEV)).sample
+    e = rel(out[[0, 15]], ref)
+    print("config-5 UNet fp8-attention rel err", e)
+    assert e < 1.2e-1

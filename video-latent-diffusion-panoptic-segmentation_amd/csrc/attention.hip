@@ -329,7 +329,23 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
 #define ATTN_ABL 0   // ablation builds only (tools/attn_ablate.sh): 1 no exp2, 2 no QK MFMA, 3 no PV MFMA
 #endif
 
-template <int DP, int QSUB, bool ONES, int NW = 4, int OCC = 8 / NW>
+// fp8 P.V (BASELINE config 5, "fp8 MFMA attention"): P (<= 2^8 under the lazy rescale) and V are
+// rounded to OCP e4m3 (v_cvt_pk_fp8_f32; V saturated to +-448) and multiplied on
+// v_mfma_f32_16x16x32_fp8_fp8 with fp32 accumulation; Q.K^T and the softmax stay bf16 / fp32.  The
+// ones column of V is exactly 1.0 in e4m3, so the denominator sums the same rounded P as the
+// numerator.  NB: the non-scaled fp8 MFMA issues at the bf16 rate on gfx950 (MI355X_MICROARCH.md,
+// Matrix cores), so this path trades accuracy for no MFMA time; it exists for config 5's numerics.
+__device__ __forceinline__ uint32_t pack_fp8x4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+__device__ __forceinline__ float sat448(float x) { return __builtin_amdgcn_fmed3f(x, -448.f, 448.f); }
+__device__ __forceinline__ uint32_t bf16x4_to_fp8x4(uint2 v) {
+  return pack_fp8x4(sat448(__uint_as_float(v.x << 16)), sat448(__uint_as_float(v.x & 0xffff0000u)),
+                    sat448(__uint_as_float(v.y << 16)), sat448(__uint_as_float(v.y & 0xffff0000u)));
+}
+
+template <int DP, int QSUB, bool ONES, int NW = 4, int OCC = 8 / NW, bool F8 = false>
 __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) {
   typedef bf16_t T;
   constexpr int ES = 2, EPC = 8;
@@ -435,6 +451,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
       }
     }
     uint2 pk[4][QSUB];                      // bf16 P^T, (kv 4g .. 4g+3 of fragment js) per lane
+    uint32_t pk8[4][QSUB];                  // F8: the same four values as e4m3 bytes
 #pragma unroll
     for (int s = 0; s < QSUB; ++s) {
       if (masked) {
@@ -476,7 +493,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 #endif
           if (!ONES) lsum += pv[r];
         }
-        pk[js][s] = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
+        if constexpr (F8) pk8[js][s] = pack_fp8x4(pv[0], pv[1], pv[2], pv[3]);
+        else pk[js][s] = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
       }
       if (!ONES) lrun[s] += lsum;
     }
@@ -490,6 +508,15 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
         const T* a0 = Vs + (32 * t + 4 * g + (lr >> 2)) * ROW + 16 * dd + 4 * (lr & 3);
         const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0)));
         const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0 + 16 * ROW)));
+        if constexpr (F8) {
+          const long va8 = (long)((uint64_t)bf16x4_to_fp8x4(lo) | ((uint64_t)bf16x4_to_fp8x4(hi) << 32));
+#pragma unroll
+          for (int s = 0; s < QSUB; ++s) {
+            const long pb8 = (long)((uint64_t)pk8[2 * t][s] | ((uint64_t)pk8[2 * t + 1][s] << 32));
+            oacc[dd][s] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(va8, pb8, oacc[dd][s], 0, 0, 0);
+          }
+          continue;
+        }
         Frag8<T> va;
         va.v = make_uint4(lo.x, lo.y, hi.x, hi.y);
 #pragma unroll
@@ -548,30 +575,30 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 
 int g_attn_waves = 0;   // 0: auto (8 when that still gives >= 256 blocks), 4 or 8: forced
 
-template <int DP, int QSUB, bool ONES>
+template <int DP, int QSUB, bool ONES, bool F8 = false>
 int launch32_cfg(const AttnArgs& a, int batch, hipStream_t s) {
   const int blocks8 = (a.nq + 128 * QSUB - 1) / (128 * QSUB) * a.heads * batch;
   if (g_attn_waves == 8 || (g_attn_waves == 0 && blocks8 >= 256)) {
     // 8 waves share every K/V tile (one 512-thread block per CU): half the LDS-DMA bytes per FLOP
     const int nblk = (a.nq + 128 * QSUB - 1) / (128 * QSUB) * a.heads * batch;
-    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 8>), dim3(nblk), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 8, 1, F8>), dim3(nblk), dim3(512), 0, s, a);
   } else {
     const int nblk = (a.nq + 64 * QSUB - 1) / (64 * QSUB) * a.heads * batch;
-    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES>), dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 4, 2, F8>), dim3(nblk), dim3(256), 0, s, a);
   }
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
 
-template <int DP, int QSUB, bool ONES, int NW, int OCC>
+template <int DP, int QSUB, bool ONES, int NW, int OCC, bool F8 = false>
 int launch_occ(const AttnArgs& a, int batch, hipStream_t s) {
   const int nblk = (a.nq + 16 * QSUB * NW - 1) / (16 * QSUB * NW) * a.heads * batch;
-  hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, NW, OCC>), dim3(nblk), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, NW, OCC, F8>), dim3(nblk), dim3(64 * NW), 0, s, a);
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
 
-template <int DP>
+template <int DP, bool F8 = false>
 int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
   // query subtiles per wave: as many as stay spill-free (the ONES variant has no l registers)
   constexpr int QS1 = DP <= 48 ? 4 : (DP <= 96 ? 2 : 1);
@@ -581,10 +608,25 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
     // CU whose phases drift apart, so one block's softmax VALU runs beside the other's MFMAs
     // (N=4096: 295 -> 265 us against one 8-wave block of 4 subtiles); needs >= 2 blocks per CU
     const int nblk2 = (a.nq + 255) / 256 * a.heads * batch;
-    if (a.d == DP - 8 && g_attn_waves == 0 && nblk2 >= 512) return launch_occ<DP, 2, true, 8, 2>(a, batch, s);
+    if (a.d == DP - 8 && g_attn_waves == 0 && nblk2 >= 512) return launch_occ<DP, 2, true, 8, 2, F8>(a, batch, s);
   }
-  if (a.d == DP - 8) return launch32_cfg<DP, QS1, true>(a, batch, s);
-  return launch32_cfg<DP, QS0, false>(a, batch, s);
+  if (a.d == DP - 8) return launch32_cfg<DP, QS1, true, F8>(a, batch, s);
+  return launch32_cfg<DP, QS0, false, F8>(a, batch, s);
+}
+
+// fp8 P.V forward (bf16 inputs with 16-byte rows only)
+int launch_fp8(const AttnArgs& a, int batch, hipStream_t s) {
+  const int dp = (a.d + 15) / 16 * 16;
+  if (a.qs % 8 || a.os % 4) return LDM_ERR_ALIGN;
+  switch (dp) {
+    case 48: return launch32_dp<48, true>(a, batch, s);
+    case 64: return launch32_dp<64, true>(a, batch, s);
+    case 80: return launch32_dp<80, true>(a, batch, s);
+    case 96: return launch32_dp<96, true>(a, batch, s);
+    case 128: return launch32_dp<128, true>(a, batch, s);
+    case 160: return launch32_dp<160, true>(a, batch, s);
+    default: return LDM_ERR_ARG;
+  }
 }
 
 int g_attn_legacy = 0;   // tuning / A-B hook: 1 forces the 16x16x16 kernel
@@ -979,6 +1021,13 @@ extern "C" int ldm_attention(const ldm_attn_params* q, ldm_stream_t stream) {
   const AttnArgs a = attn_args(q);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   return q->dtype == LDM_BF16 ? launch_bf16(a, q->batch, s) : launch_t<float>(a, q->batch, s);
+}
+
+extern "C" int ldm_attention_fp8(const ldm_attn_params* q, ldm_stream_t stream) {
+  const int st = attn_validate(q);
+  if (st != LDM_OK) return st;
+  if (q->dtype != LDM_BF16) return LDM_ERR_ARG;
+  return launch_fp8(attn_args(q), q->batch, reinterpret_cast<hipStream_t>(stream));
 }
 
 extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 || waves == 8) ? waves : 0; }

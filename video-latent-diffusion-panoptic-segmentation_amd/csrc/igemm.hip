@@ -1181,6 +1181,236 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Halo-tiled 3x3 conv (stride 1, pad 1, bf16): the K loop runs over 64-channel blocks, and
+// for each block the tile's input rows — R output rows need R + 2 input rows of W + 2 pixels
+// (the zero border included) — land in LDS ONCE; the 9 taps then read shifted views of that
+// halo instead of re-gathering the A tile 9 times (the tap-major igemm moves 9 x 128 rows of A
+// per channel block; the halo moves (R + 2)(W + 2) rows: 4.4x less A at R = 2, 7.3x at R = 4).
+// B (the weights) still streams one [160][64] tile per (channel block, tap) step.
+//   tile: BM = R x W output pixels (whole output rows of one image) x BN = 160 channels;
+//         512 threads = 8 waves as 4 (M) x 2 (N), wave tile (BM/4) x 80 of 16x16x32 MFMAs
+//   LDS : 2 halo buffers (channel block cb and cb + 1) + 2 B slots (step s and s + 1);
+//         the halo of cb + 1 is fetched in 1-KB LDS-DMA pieces spread over cb's first 7 taps
+//         (one piece per wave per tap), B of step s + 1 during step s; one barrier per step
+//   every wave issues the same instruction counts per step, so `s_waitcnt vmcnt` is exact:
+//         before step s only the halo piece issued after B(s) may stay in flight
+// ---------------------------------------------------------------------------------------
+namespace halo {
+constexpr int BN = 160, NT = 512, PIECES_PER_TAP = 8, NBS = 2;   // one 1-KB halo piece per wave per tap; 2 B slots
+constexpr int B_U4 = BN * 8;                                      // uint4 per B slot (20,480 B)
+template <int W, int R> struct Geo {
+  static constexpr int HW = W + 2, HPIX = (R + 2) * HW;          // halo row pitch, halo pixels
+  static constexpr int NP = (HPIX * 8 + 63) / 64;                // 1-KB pieces per halo
+  static constexpr int A_TAPS = (NP + PIECES_PER_TAP - 1) / PIECES_PER_TAP;
+  static constexpr int HALO_U4 = NP * 64;
+  static constexpr int SMEM_U4 = 2 * HALO_U4 + NBS * B_U4;       // W=64, R=4: 143,360 B
+};
+}  // namespace halo
+
+template <int W, int R>
+__global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
+  using namespace halo;
+  typedef bf16_t T;
+  typedef Geo<W, R> G;
+  constexpr int BM = R * W;
+  constexpr int HW = G::HW, HPIX = G::HPIX, NP = G::NP, A_TAPS = G::A_TAPS, HALO_U4 = G::HALO_U4;
+  static_assert(A_TAPS <= 7, "halo geometry");
+  constexpr int WT = BM / 4;                      // wave tile rows
+  constexpr int FM = WT / 16, FN = 5;
+  constexpr int EPI_H = BM > 128 ? 2 : 1;
+  constexpr int EPI_ROWS = BM / EPI_H;
+  constexpr int PITCH = BN + 4;
+  constexpr int EPI_U4 = (EPI_ROWS * PITCH * 4 + (NT / (BN / 8)) * (BN / 8) * (EPI_ROWS / 64) * 64 + 15) / 16;
+  constexpr int SMEM_U4 = G::SMEM_U4 > EPI_U4 ? G::SMEM_U4 : EPI_U4;
+  static_assert(SMEM_U4 * 16 <= 163840, "LDS budget");
+  __shared__ uint4 smem[SMEM_U4];
+
+  int tile;
+  {
+    const int bid = blockIdx.x, nblk = p.nblk;
+    const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
+    tile = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+  }
+  int tm, tn;
+  grouped_tile(tile, p.M / BM, p.tiles_n, p.group_m, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int b = m0 / p.hw_out;
+  const int oy0 = (m0 - b * p.hw_out) / W;
+  const int ncb = p.cin / 64;
+  const int nsteps = 9 * ncb;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int lr = lane & 15, g = lane >> 4;
+
+  const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)p.a0, 0, p.a0_bytes, kBufFlags);
+  const __amdgpu_buffer_rsrc_t ra1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.a1 ? p.a1 : p.a0), 0, p.a1 ? p.a1_bytes : 0, kBufFlags);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, p.w_bytes, kBufFlags);
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+  const unsigned lds_b = lds0 + 2 * HALO_U4 * 16;
+
+  // halo piece j (j = tap * 8 + wave, j < 56) = LDS slots [64 j, 64 j + 64): slot -> (halo pixel,
+  // stored chunk); the lane fetches the logical chunk that the XOR swizzle puts there.  Swizzle
+  // c ^ (hp & 7): the 16 lanes of each ds_read_b128 lane group hit 16 distinct 16-B bank slots for
+  // every tap offset (the tile kernels' c ^ ((r >> 1) & 7) is conflict-free only for 16-aligned
+  // row bases; at the odd tap shifts it averaged 1.67 LDS cycles per group)
+  // does this wave issue a halo piece at tap `tap` (for the next channel block)?
+  auto has_piece = [&](int tap) { return tap < A_TAPS && tap * PIECES_PER_TAP + wv < NP; };
+  auto issue_halo = [&](int cb, int tap) {
+    const int j = tap * PIECES_PER_TAP + wv;
+    const int slot = j * 64 + lane;
+    const int hp = slot >> 3, sp = slot & 7;
+    const int c = sp ^ (hp & 7);
+    const int hr = hp / HW, hx = hp - hr * HW;
+    const int iy = oy0 - 1 + hr, ix = hx - 1;
+    const bool src1 = p.c1 > 0 && cb * 64 >= p.c0;            // uniform per channel block
+    const int cs = src1 ? p.c1 : p.c0;
+    const int ch = cb * 64 - (src1 ? p.c0 : 0) + 8 * c;
+    const bool ok = hp < HPIX && (unsigned)iy < (unsigned)p.h_in && (unsigned)ix < (unsigned)W;
+    const int off = ok ? (((b * p.h_in + iy) * W + ix) * cs + ch) * 2 : kOOB;
+    const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)(((cb & 1) * HALO_U4 + j * 64) * 16));
+    if (src1) dma16(ra1, off, dst);
+    else dma16(ra0, off, dst);
+  };
+  // B tile of step s: rows n0 + r (r < 160), packed-K columns tap * cin + cb * 64 .. + 64;
+  // waves 0-3 load rows rr, rr + 64, rr + 128 (rr < 32 for the last), waves 4-7 two
+  const int rr = tid >> 3, cc = tid & 7;               // rr in [0, 64)
+  const int cl = cc ^ ((rr >> 1) & 7);                 // (rr + 64 i) >> 1 & 7 == rr >> 1 & 7
+  auto issue_b = [&](int s) {
+    const int cb = s / 9, tap = s - 9 * (s / 9);
+    const int kb = (tap * p.cin + cb * 64 + 8 * cl) * 2;
+    const unsigned base = lds_b + (unsigned)((s % NBS) * B_U4 * 16);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i == 2 && wv >= 4) break;
+      const int r = rr + 64 * i;
+      const int n = n0 + r;
+      const int off = (r < BN && n < p.n) ? n * p.kpad * 2 + kb : kOOB;
+      dma16(rw, off, __builtin_amdgcn_readfirstlane(base + (unsigned)((64 * i + 8 * wv) * 128)));
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // per-fragment halo pixel of this lane at tap (0, 0)
+  int hp0[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int ml = wm * WT + 16 * i + lr;
+    const int oyl = ml / W, ox = ml - oyl * W;
+    hp0[i] = oyl * HW + ox;
+  }
+  auto compute = [&](int s) {
+    const int cb = s / 9, tap = s - 9 * (s / 9);
+    const int ky = tap / 3, kx = tap - 3 * ky;
+    const uint4* As = smem + (cb & 1) * HALO_U4;
+    const uint4* Bs = smem + 2 * HALO_U4 + (s % NBS) * B_U4;
+    const int toff = ky * HW + kx;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      Frag8<T> af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int hp = hp0[i] + toff;
+        af[i].v = As[hp * 8 + ((ks * 4 + g) ^ (hp & 7))];
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * 80 + j * 16 + lr;
+        bfr[j].v = Bs[r * 8 + swz(r, ks * 4 + g)];
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) mma_k32(acc[i][j], bfr[j], af[i]);
+    }
+  };
+
+  // prologue: the whole halo of channel block 0 and B of step 0
+#pragma unroll
+  for (int t = 0; t < A_TAPS; ++t)
+    if (has_piece(t)) issue_halo(0, t);
+  issue_b(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int cb = s / 9, tap = s - 9 * (s / 9);
+    if (s > 0) {
+      // issued by this wave after B(s) (at step s - 1): the halo piece of step s - 1, if any.
+      // (A deeper, 3-slot B ring measured slower: 68 -> 74 us on the 64x64 320-channel conv.)
+      const int pt = tap == 0 ? 8 : tap - 1;
+      const int pcb = tap == 0 ? cb - 1 : cb;
+      if (pcb + 1 < ncb && has_piece(pt)) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_barrier" ::: "memory");
+    }
+    if (s + 1 < nsteps) issue_b(s + 1);
+    if (cb + 1 < ncb && has_piece(tap)) issue_halo(cb + 1, tap);
+    compute(s);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  // ---- fused epilogue (LDS-staged, EPI_H row halves; waves wm with (wm * WT) / EPI_ROWS == h)
+  float* stage = reinterpret_cast<float*>(smem);
+  float* red = stage + EPI_ROWS * PITCH;
+  const bool fast = fast_epilogue_ok(p);
+  auto raw = [&](int r, int c4, float* v) {
+    const float4 x = *reinterpret_cast<const float4*>(stage + r * PITCH + 4 * c4);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  };
+#pragma unroll
+  for (int h = 0; h < EPI_H; ++h) {
+    __syncthreads();
+    if ((wm * WT) / EPI_ROWS == h) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ml = wm * WT - h * EPI_ROWS + i * 16 + lr;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int nl = wn * 80 + j * 16 + 4 * g;
+          *reinterpret_cast<float4*>(stage + ml * PITCH + nl) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+        }
+      }
+    }
+    __syncthreads();
+    const int mh = m0 + h * EPI_ROWS;
+    if (fast && fast_temb_ok(p, mh, EPI_ROWS)) epilogue_fast<EPI_ROWS, BN, NT>(p, mh, n0, stage, PITCH, red);
+    else epilogue_rows<T, EPI_ROWS, BN, NT>(p, mh, n0, raw, red);
+  }
+}
+
+// halo plan: bf16 3x3 stride-1 conv, no upsample, 64-channel-aligned sources, an output width
+// the kernel is instantiated for, whole output rows per tile
+int g_halo_mode = 0;   // tuning hook: 0 planner, 1 never, 2 whenever legal
+bool halo_legal(const ldm_conv_params* q, int es) {
+  if (es != 2 || q->ksize != 3 || q->stride != 1 || q->upsample || q->pad_mode != 0) return false;
+  if (q->c0 % 64 || q->c1 % 64 || q->kpad != 9 * (q->c0 + q->c1)) return false;
+  if (q->h_in != q->h_out || q->w_in != q->w_out) return false;
+  if (q->out_layout != LDM_OUT_NHWC || q->out_f32) return false;
+  const int W = q->w_out;
+  const int R = W == 64 ? 4 : (W == 32 ? 4 : 0);
+  return R && q->h_out % R == 0;
+}
+
+int launch_halo(ConvArgs a, hipStream_t s) {
+  a.tiles_n = (a.n + halo::BN - 1) / halo::BN;
+  const int bm = a.w_out * 4;
+  a.nblk = (a.M / bm) * a.tiles_n;
+  if (a.w_out == 64) hipLaunchKernelGGL((conv3_halo_kernel<64, 4>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  else hipLaunchKernelGGL((conv3_halo_kernel<32, 4>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
 int g_force_stages = 0;   // tuning hook: 1 register-staged operands, 3 / 4 ring depth, 0 planner
 
 template <typename T, int BM, int BN, int NS = 2>
@@ -1395,6 +1625,15 @@ bool is_mixed(const ldm_conv_params* q, int es) {
   return q->c1 > 0 && (q->c0 % bk || q->c1 % bk);
 }
 
+// Planner (opbench at the UNet shapes, B=8; igemm -> halo, us): 64 wide: 320->320 76 -> 69,
+// [640||320]->320 191 -> 168; 32 wide: 640->640 84 -> 76, 320->640 45 -> 44, but [1280||640]->640
+// 191 -> 206 (30 channel blocks on the 128-row halo tile lose to the tap-major 128x160 tiles)
+bool use_halo_plan(const ldm_conv_params* q, int es, bool mixed) {
+  if (g_halo_mode == 1 || mixed || g_force_bm || !halo_legal(q, es)) return false;
+  if (g_halo_mode == 2) return true;
+  return q->n % halo::BN == 0 && (q->w_out == 64 || (q->w_out == 32 && q->c0 + q->c1 <= 960));
+}
+
 }  // namespace
 
 extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
@@ -1409,6 +1648,7 @@ extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
 
 int g_group_m = 8;
 extern "C" void ldm_conv2d_set_raster_group(int g) { g_group_m = g >= 1 ? g : 8; }
+extern "C" void ldm_conv2d_set_halo(int mode) { g_halo_mode = (mode == 1 || mode == 2) ? mode : 0; }
 extern "C" void ldm_conv2d_force_stages(int stages) {
   g_force_stages = (stages == 1 || stages == 3 || stages == 4) ? stages : 0;   // 1: register-staged operands
 }
@@ -1417,7 +1657,9 @@ extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   int es = 0;
   if (validate(q, &es) != LDM_OK) return 0;
   const int M = q->batch * q->h_out * q->w_out;
-  const Plan pl = make_plan(q, M, es, is_mixed(q, es));
+  const bool mixed = is_mixed(q, es);
+  if (use_halo_plan(q, es, mixed)) return 0;
+  const Plan pl = make_plan(q, M, es, mixed);
   return pl.ksplit > 1 ? (size_t)pl.ksplit * M * q->n * sizeof(float) : 0;
 }
 
@@ -1429,7 +1671,8 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   const int cin = q->c0 + q->c1;
   const int M = q->batch * q->h_out * q->w_out;
   const bool mixed = is_mixed(q, es);
-  const Plan pl = make_plan(q, M, es, mixed);
+  const bool use_halo = use_halo_plan(q, es, mixed);
+  const Plan pl = use_halo ? Plan{0, 0, 1} : make_plan(q, M, es, mixed);
   if (pl.ksplit > 1) {
     const size_t need = (size_t)pl.ksplit * M * q->n * sizeof(float);
     if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;
@@ -1461,6 +1704,7 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.partial = static_cast<float*>(q->workspace);
   a.gn_part = reinterpret_cast<float2*>(q->gn_partial);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (use_halo) return launch_halo(a, s);
   if (pl.bm == 256) return launch_big(a, s);
   const int stages = g_force_stages ? g_force_stages : pl.stages;
   return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, s, pl.bm, pl.bn, stages) : launch_t<float>(a, s, pl.bm, pl.bn);

@@ -464,6 +464,15 @@ class UNet(nn.Module):
         self._dplan = D
         return D
 
+    @property
+    def attention_fp8(self):
+        return getattr(self, "_attention_fp8", False)
+
+    def set_attention_fp8(self, enabled=True):
+        """BASELINE config 5: self-attention P.V on the e4m3 MFMA (ldm_attention_fp8) when the
+        compute dtype is bf16; an inference option (the training path keeps bf16)."""
+        self._attention_fp8 = bool(enabled)
+
     def invalidate_packed(self):
         """Drop the packed weights (call after an in-place optimizer update that bypasses
         torch's version counter, e.g. the fused AdamW of ldmseg.trainers)."""
@@ -492,7 +501,8 @@ class UNet(nn.Module):
         n = K.layer_norm(h, *p["ln1"], 1e-5)
         qkv = K.linear(p["qkv"], n)                                      # [B, N, 3C]
         heads, dh = p["heads"], p["dim_head"]
-        a = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, dh, N, N, 3 * C, 3 * C, 3 * C)
+        a = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, dh, N, N, 3 * C, 3 * C, 3 * C,
+                        fp8=self.attention_fp8 and qkv.dtype == torch.bfloat16)
         h = K.linear(p["out1"], a, residual=h, out=h)
         if p["attn2"] is not None and ehs is not None:
             q2 = p["attn2"]

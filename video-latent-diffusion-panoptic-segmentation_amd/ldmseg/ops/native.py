@@ -62,7 +62,9 @@ EXPORTS = {
     "ldm_conv2d_force_plan": (None, [_i, _i, _i]),
     "ldm_conv2d_force_stages": (None, [_i]),
     "ldm_conv2d_set_raster_group": (None, [_i]),
+    "ldm_conv2d_set_halo": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
+    "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_group_norm_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
     "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _i, _vp]),
     "ldm_layer_norm": (_i, [_vp, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp]),
@@ -418,6 +420,11 @@ def set_conv_raster_group(group_m=8):
     load_library().ldm_conv2d_set_raster_group(int(group_m))
 
 
+def set_conv_halo(mode=0):
+    """Tuning hook: halo-tiled 3x3 kernel — 0 planner, 1 never, 2 whenever legal."""
+    load_library().ldm_conv2d_set_halo(int(mode))
+
+
 def force_conv_plan(bm=0, bn=0, ksplit=1):
     """Tuning hook: force ldm_conv2d's tile plan (bm=256 -> large-tile bf16 kernel); bm=0 resets."""
     load_library().ldm_conv2d_force_plan(int(bm), int(bn), int(ksplit))
@@ -438,7 +445,9 @@ def linear(pc: PackedConv, x, **kw):
 # ======================================================================================
 # attention / norms
 # ======================================================================================
-def attention(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_stride, out=None, scale=None):
+def attention(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_stride, out=None, scale=None,
+              fp8=False):
+    """fp8=True: ldm_attention_fp8 (P.V on the e4m3 MFMA; bf16 inputs only)."""
     lib = load_library()
     _gpu(q, k, v, out)
     C = heads * head_dim
@@ -453,7 +462,12 @@ def attention(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_
     p = AttnParams(_ptr(q), _ptr(k), _ptr(v), _ptr(out), q_stride, k_stride, v_stride, C, batch, heads, head_dim,
                    n_q, n_kv, float(scale if scale is not None else head_dim ** -0.5), dtype_code(q.dtype))
     ev = _prof_start()
-    _check(lib.ldm_attention(ctypes.byref(p), _stream(q)), "ldm_attention")
+    if fp8:
+        if q.dtype != torch.bfloat16:
+            raise TypeError("fp8 attention takes bf16 q/k/v")
+        _check(lib.ldm_attention_fp8(ctypes.byref(p), _stream(q)), "ldm_attention_fp8")
+    else:
+        _check(lib.ldm_attention(ctypes.byref(p), _stream(q)), "ldm_attention")
     _prof_stop(ev, "attention", 4.0 * batch * heads * n_q * n_kv * head_dim,
                (2 * batch * n_q * C + 2 * batch * n_kv * C) * q.element_size(), f"N={n_q} L={n_kv} d={head_dim}")
     return out
