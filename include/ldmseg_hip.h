@@ -78,10 +78,18 @@ typedef struct {
   int out_f32;             /* 1: out is fp32 regardless of dtype */
   void* workspace;         /* split-K fp32 slab, >= ldm_conv2d_workspace_bytes(p) bytes (or NULL if 0) */
   int64_t workspace_bytes;
-  float* gn_partial;       /* optional: per 64-row chunk, per channel (sum, sumsq) of the output,
-                              [M/64][n] float2 — the GroupNorm statistics input (NHWC, M % 64 == 0) */
+  double* gn_partial;      /* optional: GroupNorm statistics of the output, [batch][gn_slots][n / gn_unit][2]
+                              fp64 (sum, sumsq) accumulators, one per gn_unit consecutive channels,
+                              that the epilogue ADDS to (atomically, one fp32 partial per unit and
+                              tile, spread over gn_slots copies by tile row): zero them first
+                              (NHWC, h_out*w_out % 64 == 0) */
   int pad_mode;            /* 0: zero padding ksize/2 on every side; 1: diffusers Downsample2D(padding=0):
                               F.pad (0, 1, 0, 1) then an unpadded conv (AutoencoderKL encoder) */
+  int gn_unit;             /* channels per gn_partial accumulator (n % gn_unit == 0; 0 means 1).  Any
+                              GroupNorm whose group size and concat offset are multiples of it can
+                              consume them — 10 serves every SD UNet GroupNorm, concats included */
+  int gn_slots;            /* copies of the accumulators (0 means 1): same-address atomics serialise,
+                              so the row tiles of one batch are spread over the slots */
 } ldm_conv_params;
 
 /* Deep-K / few-tile shapes are split over K into an fp32 slab; this returns its size (0: none). */
@@ -143,20 +151,24 @@ int ldm_attention_bwd(const ldm_attn_params* p, const void* o, const void* d_o, 
  * concatenated sources (the up-block [hidden || skip] concat is never materialised).
  * Replaces: ResnetBlock2D norm1/norm2 + SiLU (eps 1e-5), Transformer2DModel.norm (eps 1e-6),
  * conv_norm_out + conv_act (unet.py:428-430), GeneralVAESeg GroupNorm (vae.py:163,235).
- * stats0/stats1: the per-64-pixel-chunk channel (sum, sumsq) partials [batch*hw/64][c_i] float2
- * that ldm_conv2d's epilogue wrote for x0 / x1 (gn_partial), or NULL to compute them here.
+ * stats0/stats1: the fp64 (sum, sumsq) accumulators [batch][stats_slots][c_i / stats_unit][2]
+ * that ldm_conv2d's epilogue summed for x0 / x1 (gn_partial, gn_unit = stats_unit, gn_slots =
+ * stats_slots), or NULL to compute them here (an extra read of the tensor).  stats_unit must
+ * divide c0 and the group size.
+ * One kernel when both are given: every block reduces its batch's accumulators to per-group
+ * mean / rstd in LDS while its first rows are in flight, then streams its rows.
  * workspace: >= ldm_group_norm_workspace_bytes(batch, hw, c0 + c1) bytes of device memory.
  * ------------------------------------------------------------------------------------- */
 size_t ldm_group_norm_workspace_bytes(int batch, int hw, int channels);
 int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
                    const float* gamma, const float* beta, float eps, int act, void* out,
-                   const float* stats0, const float* stats1, void* workspace, int dtype,
-                   ldm_stream_t stream);
+                   const double* stats0, const double* stats1, int stats_unit, int stats_slots, void* workspace,
+                   int dtype, ldm_stream_t stream);
 /* Training forward: also stores (mean, rstd) per (batch, group) [batch][groups] float2. */
 int ldm_group_norm_ex(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
                       const float* gamma, const float* beta, float eps, int act, void* out,
-                      const float* stats0, const float* stats1, void* workspace, float* save_mean_rstd,
-                      int dtype, ldm_stream_t stream);
+                      const double* stats0, const double* stats1, int stats_unit, int stats_slots,
+                      void* workspace, float* save_mean_rstd, int dtype, ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_layer_norm — LayerNorm over the channel dimension of [rows][c] (NHWC pixels or tokens).

@@ -79,7 +79,8 @@ def test_conv2d(case, dt):
 
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("B,H,C,Co,G,split", [(2, 32, 128, 320, 32, False), (8, 8, 1280, 1280, 32, True),
-                                               (1, 16, 64, 64, 16, False)])
+                                               (1, 16, 64, 64, 16, False),
+                                               (2, 16, 64, 320, 64, False)])   # group 5 ch: unit 10 unusable
 def test_conv_epilogue_groupnorm_stats(B, H, C, Co, G, split, dt):
     """Producer-epilogue (sum, sumsq) partials feed GroupNorm: no statistics pass, same result.
     Also across a concat whose second half carries its own producer statistics."""
@@ -101,6 +102,32 @@ def test_conv_epilogue_groupnorm_stats(B, H, C, Co, G, split, dt):
     out2 = K.group_norm(y, B, H * H, G, gam2.to(DEV), bet2.to(DEV), 1e-6, x1=y2)
     ref2 = F.group_norm(torch.cat([y_ref, F.silu(y_ref)], 1), G, gam2, bet2, 1e-6)
     assert rel_err(out2.view(B, H, H, -1).permute(0, 3, 1, 2), ref2) < (2e-4 if dt == torch.float32 else 3e-2)
+
+
+@pytest.mark.parametrize("split", [False, True])
+def test_conv_groupnorm_accumulators_and_arena(split):
+    """The epilogue's fp64 accumulators hold each (batch, unit of gn_unit channels)'s (sum, sumsq)
+    of the STORED output; inside K.gn_arena the second forward with the same key takes them from one zeroed
+    buffer and gives the same sums."""
+    torch.manual_seed(9)
+    B, H, C, Co = (8, 8, 1280, 1280) if split else (2, 64, 128, 320)     # 64x64: 8 slots
+    x = torch.randn(B, H, H, C).to(DEV, torch.bfloat16)
+    pc = K.PackedConv((torch.randn(Co, C, 3, 3) / (3 * C ** 0.5)).to(DEV), torch.randn(Co).to(DEV), torch.bfloat16)
+    sums = []
+    for it in range(3):
+        with K.gn_arena(("test_arena", split), DEV):
+            y = K.conv2d(pc, x, B, H, H, gn_stats=True)
+            y2 = K.conv2d(pc, x, B, H, H, act=K.ACT_SILU, gn_stats=True)
+        a, a2 = K.gn_stats_of(y), K.gn_stats_of(y2)
+        U, S = K.gn_unit_for(Co), K.gn_slots_for(H * H)
+        assert a.dtype == torch.float64 and a.shape == (B, S, Co // U, 2)
+        if it > 0:                                 # arena slices: one storage for both
+            assert a.untyped_storage().data_ptr() == a2.untyped_storage().data_ptr()
+        yd = y.double().view(B, H * H, Co // U, U)
+        ref = torch.stack([yd.sum((1, 3)), (yd * yd).sum((1, 3))], -1)
+        assert torch.allclose(a.sum(1), ref, rtol=1e-5, atol=1e-3)
+        sums.append(a.clone())
+    assert torch.allclose(sums[0], sums[2], rtol=1e-9, atol=1e-9)
 
 
 @pytest.mark.parametrize("dt", DTYPES)

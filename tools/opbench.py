@@ -60,7 +60,8 @@ def attn_case(B, N, C, heads=8, legacy=False, waves=0):
 def gn_case(B, HW, C, stats):
     x = torch.randn(B, HW, C, device=DEV).to(BF)
     if stats:
-        setattr(x, K.GN_PART_ATTR, torch.zeros(B * HW // 64, C, 2, device=DEV))
+        setattr(x, K.GN_PART_ATTR, torch.zeros(B, K.gn_slots_for(HW), C // K.gn_unit_for(C), 2, dtype=torch.float64,
+                                               device=DEV))
     gam, bet = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
 
     def run():
@@ -86,6 +87,9 @@ def panoptic_case(B, Kc, H, W):
 
 CASES = {
     "conv3_l0_320": lambda: conv_case(8, 64, 64, 320, 320, temb=True, stats=True),
+    "conv3_l0_320_ns": lambda: conv_case(8, 64, 64, 320, 320, temb=True),
+    "conv3_up_l0_960_ns": lambda: conv_case(8, 64, 64, 960, 320, c1=320, residual=True),
+    "conv3_l1_640_ns": lambda: conv_case(8, 32, 32, 640, 640, temb=True),
     "conv3_l1_640": lambda: conv_case(8, 32, 32, 640, 640, temb=True, stats=True),
     "conv3_l2_1280": lambda: conv_case(8, 16, 16, 1280, 1280, temb=True, stats=True),
     "conv3_l3_1280": lambda: conv_case(8, 8, 8, 1280, 1280, temb=True, stats=True),

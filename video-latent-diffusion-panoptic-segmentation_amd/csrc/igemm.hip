@@ -47,7 +47,10 @@ struct ConvArgs {
   int mixed_src;      // the concat boundary is not K-tile aligned: per-lane source select
   int ksplit;         // > 1: write fp32 partials to `partial` [ksplit][M][n]
   float* partial;
-  float2* gn_part;    // optional [M/64][n] (sum, sumsq) of the final output values
+  double* gn_part;    // optional [batch][gn_slots][n / gn_unit][2] fp64 (sum, sumsq) accumulators of
+                      // the stored output (zeroed by the caller; each tile adds one fp32 partial
+                      // per gn_unit-channel unit atomically, into slot (tile row index) % gn_slots)
+  int gn_unit, gn_slots;
   int tap_inner;      // K tiles visited channel-block-major, taps inner (see k_state)
   int group_m;        // M panels per raster group (grouped_tile); 1 = plain row-major tiles
 };
@@ -212,6 +215,76 @@ __device__ __forceinline__ void finish4(const ConvArgs& p, int b, int pix, int m
   }
 }
 
+// Floats of the epilogue's GroupNorm scratch `red`: one record of HALVES x CPC (sum, sumsq)
+// pairs per thread, padded by 4 (CPC 8: ds_write_b128) or 2 (CPC 4: ds_write_b64) floats so
+// consecutive threads' records start in different banks (unpadded, a 64-float record put all 16
+// lanes of a b128 write in one bank group: a 16-way conflict).
+template <int NT, int COLS, int ROWS, int CPC>
+constexpr int gn_red_stride() { return (ROWS >= 64 ? ROWS / 64 : 1) * CPC * 2 + (CPC == 8 ? 4 : 2); }
+template <int NT, int COLS, int ROWS, int CPC>
+constexpr int gn_red_floats() { return (NT / (COLS / CPC)) * (COLS / CPC) * gn_red_stride<NT, COLS, ROWS, CPC>(); }
+
+// GroupNorm statistics: a run of 64-row chunks' fp32 (sum, sumsq) of one gn_unit-channel unit
+// into the batch's fp64 accumulators, slot `slot` of gn_slots (the GroupNorm consumer sums the
+// slots and finalises per-group mean / rstd).  Same-address atomics serialise at the memory-side
+// atomic unit, so the slots spread the tiles of one batch over gn_slots copies.
+__device__ __forceinline__ void gn_accumulate(const ConvArgs& p, int batch, int slot, int unit, float a, float b) {
+  double* acc = p.gn_part + (((int64_t)batch * p.gn_slots + slot) * (p.n / p.gn_unit) + unit) * 2;
+  unsafeAtomicAdd(acc, (double)a);
+  unsafeAtomicAdd(acc + 1, (double)b);
+}
+
+// Final step of the epilogue's GroupNorm statistics.  On entry thread `tid` holds the (sum,
+// sumsq) over the tile rows of one 64-row chunk half for the elements e = tid + i * NT,
+// e = (c * HALVES + hh) * CPC + k <-> tile column CPC * c + k.  They are parked in `red` (all
+// earlier reads of it are complete), then every gn_unit-channel unit of the tile is summed over
+// its columns and over the halves of one batch, and added to its accumulator: one atomic pair
+// per (unit, batch) of the tile, not per (channel, 64-row chunk) (a unit split by a tile edge
+// gets one partial from each tile).
+template <int HALVES, int CPC, int COLS, int NT, int EPT>
+__device__ __forceinline__ void gn_units_out(const ConvArgs& p, int m0, int n0, int tid, const float* ra,
+                                             const float* rb, float* red) {
+  constexpr int NE = (COLS / CPC) * HALVES * CPC;
+#ifdef LDM_ABL_GN_NO_UNITS   // ablation build: per-channel reduction kept, unit sums / atomics dropped
+  if (ra[0] == 12345.f) red[tid] = rb[0];
+  return;
+#endif
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + i * NT;
+    if (e < NE) { red[2 * e] = ra[i]; red[2 * e + 1] = rb[i]; }
+  }
+  __syncthreads();
+  const int U = p.gn_unit;
+  const int nend = min(n0 + COLS, p.n);
+  const int ufirst = n0 / U, nu = (nend - 1) / U - ufirst + 1;
+  const int c0 = m0 >> 6;                                  // first chunk of this epilogue
+  const int slot = (c0 / HALVES) % p.gn_slots;
+  for (int t = tid; t < nu; t += NT) {
+    const int uu = ufirst + t;
+    const int cb = max(uu * U, n0) - n0, ce = min((uu + 1) * U, nend) - n0;
+    float a = 0.f, b = 0.f;
+    int bat = (c0 * 64) / p.hw_out;
+    for (int hh = 0; hh < HALVES; ++hh) {
+      const int chunk = c0 + hh;
+      if (chunk * 64 >= p.M) break;
+      const int cb_bat = (chunk * 64) / p.hw_out;
+      if (cb_bat != bat) {                                 // the tile crosses into the next batch
+        gn_accumulate(p, bat, slot, uu, a, b);
+        a = b = 0.f;
+        bat = cb_bat;
+      }
+      for (int col = cb; col < ce; ++col) {
+        const int e = ((col / CPC) * HALVES + hh) * CPC + col % CPC;
+        a += red[2 * e];
+        b += red[2 * e + 1];
+      }
+    }
+    gn_accumulate(p, bat, slot, uu, a, b);
+  }
+}
+
 // Phase 2 of the epilogue, shared by the fused path (raw values staged in LDS) and the
 // split-K reduction (raw values summed from the fp32 slab).  `raw(r, c4, v)` fills 4 raw
 // values of local row r, local 4-channel chunk c4.  Rows [0, ROWS), channels [0, COLS),
@@ -220,7 +293,8 @@ __device__ __forceinline__ void finish4(const ConvArgs& p, int b, int pix, int m
 // and rows go in groups of GP whose raw values and residuals are all fetched before any is
 // finished — the global loads of a group overlap instead of forming a latency chain.
 // With gn_part set, per-channel (sum, sumsq) over each 64-row chunk of the stored values
-// is reduced through `red` ([RP][CW][ROWS/64][4][2] floats) and written to gn_part.
+// is reduced through `red` ([RP][CW][ROWS/64][4][2] floats) and added to the chunk's batch
+// accumulators in gn_part (fp64 atomics; a chunk never spans two batches: hw % 64 == 0).
 template <typename T, int ROWS, int COLS, int NT, typename RawFn>
 __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0, RawFn raw, float* red) {
   constexpr int CW = COLS / 4;           // chunks per row
@@ -228,6 +302,7 @@ __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0,
   constexpr int NP = (ROWS + RP - 1) / RP;
   constexpr int GP = 4;                  // rows in flight per thread
   constexpr int HALVES = ROWS / 64 > 0 ? ROWS / 64 : 1;
+  constexpr int RS = gn_red_stride<NT, COLS, ROWS, 4>();
   const int tid = threadIdx.x;
   const int c4 = tid % CW, r0 = tid / CW;
   const int N = p.n;
@@ -333,29 +408,37 @@ __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0,
     }
   }
   if (!stats) return;
+#ifdef LDM_ABL_GN_ROWS_ONLY  // ablation build: row sums kept, no block reduction / atomics
+  if (s[0][0] == 12345.f) red[tid] = sq[0][0];
+  return;
+#endif
   __syncthreads();
   if (r0 < RP) {
 #pragma unroll
     for (int hh = 0; hh < HALVES; ++hh)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 0] = s[hh][k];
-        red[(((r0 * CW + c4) * HALVES + hh) * 4 + k) * 2 + 1] = sq[hh][k];
+        red[(r0 * CW + c4) * RS + (hh * 4 + k) * 2 + 0] = s[hh][k];
+        red[(r0 * CW + c4) * RS + (hh * 4 + k) * 2 + 1] = sq[hh][k];
       }
   }
   __syncthreads();
-  for (int e = tid; e < CW * HALVES * 4; e += NT) {
+  constexpr int EPT = (CW * HALVES * 4 + NT - 1) / NT;
+  float ra[EPT], rb[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + i * NT;
     const int k = e & 3, hh = (e >> 2) % HALVES, c = e / (4 * HALVES);
-    const int nn = n0 + 4 * c + k;
-    const int chunk = (m0 >> 6) + hh;
-    if (nn >= N || chunk * 64 >= p.M) continue;
     float a = 0.f, b = 0.f;
-    for (int rg = 0; rg < RP; ++rg) {
-      a += red[(((rg * CW + c) * HALVES + hh) * 4 + k) * 2 + 0];
-      b += red[(((rg * CW + c) * HALVES + hh) * 4 + k) * 2 + 1];
-    }
-    p.gn_part[(int64_t)chunk * N + nn] = make_float2(a, b);
+    if (e < CW * HALVES * 4 && n0 + 4 * c + k < N)
+      for (int rg = 0; rg < RP; ++rg) {
+        a += red[(rg * CW + c) * RS + (hh * 4 + k) * 2 + 0];
+        b += red[(rg * CW + c) * RS + (hh * 4 + k) * 2 + 1];
+      }
+    ra[i] = a;
+    rb[i] = b;
   }
+  gn_units_out<HALVES, 4, COLS, NT, EPT>(p, m0, n0, tid, ra, rb, red);
 }
 
 // Fast epilogue for the common bf16 cases (NHWC with bias / time embedding / SiLU / residual /
@@ -434,6 +517,7 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
   constexpr int RP = NT / CW;                  // rows per pass
   constexpr int NP = (ROWS + RP - 1) / RP;
   constexpr int HALVES = ROWS >= 64 ? ROWS / 64 : 1;
+  constexpr int RS = gn_red_stride<NT, COLS, ROWS, 8>();
   const int c8 = tid % CW, r0 = tid / CW;
   const int n = n0 + 8 * c8;
   const bool act = r0 < RP && n < N;
@@ -518,29 +602,37 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
     }
   }
   if (!stats) return;
+#ifdef LDM_ABL_GN_ROWS_ONLY  // ablation build: row sums kept, no block reduction / atomics
+  if (s[0][0] == 12345.f) red[tid] = sq[0][0];
+  return;
+#endif
   __syncthreads();                             // every stage read is done: red may alias it
   if (r0 < RP) {
 #pragma unroll
     for (int hh = 0; hh < HALVES; ++hh)
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        red[((r0 * CW + c8) * HALVES + hh) * 16 + 2 * k] = s[hh][k];
-        red[((r0 * CW + c8) * HALVES + hh) * 16 + 2 * k + 1] = sq[hh][k];
+        red[(r0 * CW + c8) * RS + hh * 16 + 2 * k] = s[hh][k];
+        red[(r0 * CW + c8) * RS + hh * 16 + 2 * k + 1] = sq[hh][k];
       }
   }
   __syncthreads();
-  for (int e = tid; e < CW * HALVES * 8; e += NT) {
+  constexpr int EPT = (CW * HALVES * 8 + NT - 1) / NT;
+  float ra[EPT], rb[EPT];
+#pragma unroll
+  for (int i = 0; i < EPT; ++i) {
+    const int e = tid + i * NT;
     const int k = e & 7, hh = (e >> 3) % HALVES, c = e / (8 * HALVES);
-    const int nn = n0 + 8 * c + k;
-    const int chunk = (m0 >> 6) + hh;
-    if (nn >= N || chunk * 64 >= p.M) continue;
     float a = 0.f, b = 0.f;
-    for (int rg = 0; rg < RP; ++rg) {
-      a += red[((rg * CW + c) * HALVES + hh) * 16 + 2 * k];
-      b += red[((rg * CW + c) * HALVES + hh) * 16 + 2 * k + 1];
-    }
-    p.gn_part[(int64_t)chunk * N + nn] = make_float2(a, b);
+    if (e < CW * HALVES * 8 && n0 + 8 * c + k < N)
+      for (int rg = 0; rg < RP; ++rg) {
+        a += red[(rg * CW + c) * RS + hh * 16 + 2 * k];
+        b += red[(rg * CW + c) * RS + hh * 16 + 2 * k + 1];
+      }
+    ra[i] = a;
+    rb[i] = b;
   }
+  gn_units_out<HALVES, 8, COLS, NT, EPT>(p, m0, n0, tid, ra, rb, red);
 }
 
 // Split-K: raw fp32 accumulators of a staged [ROWS][pitch] tile -> this split's slab
@@ -584,6 +676,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   constexpr int EPI_ROWS = BM / EPI_H;
   constexpr int SMEM_EPI = (EPI_ROWS * PITCH + 3) / 4;   // uint4
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  static_assert(gn_red_floats<256, BN, EPI_ROWS, 4>() <= SMEM * 4 &&
+                (EPI_ROWS < 64 || gn_red_floats<256, BN, EPI_ROWS, 8>() <= SMEM * 4), "GN scratch exceeds LDS");
   __shared__ uint4 smem[SMEM];
 
   // ---- tile / split assignment; XCD-aware: blocks b and b+8 share an XCD, give each XCD a
@@ -914,6 +1008,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) {
   constexpr int ROWS = 64, COLS = 128, PITCH = COLS + 4, RPQ = 256 / (COLS / 4);   // 8 rows per pass
   __shared__ float stage[ROWS * PITCH];   // also the statistics scratch of either epilogue
+  static_assert(gn_red_floats<256, COLS, ROWS, 8>() <= ROWS * PITCH && gn_red_floats<256, COLS, ROWS, 4>() <= ROWS * PITCH,
+                "GN scratch exceeds the stage");
   const int tiles_n = (p.n + 127) / 128;
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
   const int m0 = tm * 64, n0 = tn * 128;
@@ -982,7 +1078,8 @@ constexpr int STAGE_U4 = (BM + BN) * 8;          // uint4 per ring stage (53,248
 constexpr int NSTAGE = 3;
 constexpr int EPI_ROWS = 128;                      // epilogue staged in two row halves
 constexpr int PITCH = BN + 4;
-constexpr int RED_FLOATS = (NT / (BN / 8)) * (BN / 8) * (EPI_ROWS / 64) * 16;   // epilogue_fast layout (>= epilogue_rows')
+constexpr int RED_FLOATS = gn_red_floats<NT, BN, EPI_ROWS, 8>() > gn_red_floats<NT, BN, EPI_ROWS, 4>()
+                               ? gn_red_floats<NT, BN, EPI_ROWS, 8>() : gn_red_floats<NT, BN, EPI_ROWS, 4>();
 static_assert(EPI_ROWS * PITCH + RED_FLOATS <= NSTAGE * STAGE_U4 * 4, "epilogue does not fit the ring");
 }  // namespace big
 
@@ -1221,7 +1318,9 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
   constexpr int EPI_H = BM > 128 ? 2 : 1;
   constexpr int EPI_ROWS = BM / EPI_H;
   constexpr int PITCH = BN + 4;
-  constexpr int EPI_U4 = (EPI_ROWS * PITCH * 4 + (NT / (BN / 8)) * (BN / 8) * (EPI_ROWS / 64) * 64 + 15) / 16;
+  constexpr int RED_F = gn_red_floats<NT, BN, EPI_ROWS, 8>() > gn_red_floats<NT, BN, EPI_ROWS, 4>()
+                           ? gn_red_floats<NT, BN, EPI_ROWS, 8>() : gn_red_floats<NT, BN, EPI_ROWS, 4>();
+  constexpr int EPI_U4 = (EPI_ROWS * PITCH * 4 + RED_F * 4 + 15) / 16;
   constexpr int SMEM_U4 = G::SMEM_U4 > EPI_U4 ? G::SMEM_U4 : EPI_U4;
   static_assert(SMEM_U4 * 16 <= 163840, "LDS budget");
   __shared__ uint4 smem[SMEM_U4];
@@ -1537,8 +1636,15 @@ Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
   // deep K over fewer tiles: 128x160 split to ~512 blocks (<= 8 ways; the coalesced fp32 slab
   // stays small enough at the 16x16 / 8x8 levels)
   if (es == 2 && waste_ok && split_ok && nk >= 64) {
+    // the 8x8 level (M = 512 at B = 8): 3x3 1280 -> 1280 (nk 180) 43.7 -> 38.6 us on 64x160 x 8
+    // splits; the 2560-channel concat conv (nk 360) 65.9 -> 57.5 us on 128x160 x 16 splits
+    if (M <= 512 && nk >= 128 && nk < 256 && !mixed_src) {
+      pl.bm = 64; pl.bn = 160; pl.ksplit = 8;
+      return pl;
+    }
     pl.bm = 128; pl.bn = 160;
-    pl.ksplit = std::max(1, std::min(std::min(8, nk / 16), (512 + t128 / 2) / t128));
+    const int kcap = (M <= 512 && nk >= 256) ? 16 : 8;
+    pl.ksplit = std::max(1, std::min(std::min(kcap, nk / 16), (512 + t128 / 2) / t128));
     // <= 256 blocks: one per CU, so a 3-stage ring costs no occupancy (8x8 level: -5 %)
     if (t128 * pl.ksplit <= 256 && !mixed_src) pl.stages = 3;
     return pl;
@@ -1609,6 +1715,7 @@ int validate(const ldm_conv_params* q, int* es_out) {
   if (q->out_layout < 0 || q->out_layout > 3) return LDM_ERR_ARG;
   const int64_t M64 = (int64_t)q->batch * q->h_out * q->w_out;
   if (q->gn_partial && (M64 % 64 || (q->h_out * q->w_out) % 64 || q->out_layout != LDM_OUT_NHWC)) return LDM_ERR_ARG;
+  if (q->gn_partial && (q->gn_unit < 0 || (q->gn_unit > 0 && q->n % q->gn_unit) || q->gn_slots < 0)) return LDM_ERR_ARG;
   const int64_t a0_bytes = (int64_t)q->batch * q->h_in * q->w_in * q->c0 * es;
   const int64_t a1_bytes = (int64_t)q->batch * q->h_in * q->w_in * q->c1 * es;
   const int64_t w_bytes = (int64_t)q->n * q->kpad * es;
@@ -1702,7 +1809,9 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.tap_inner = (!mixed && q->ksize > 1 && cin % bk == 0 && q->c0 % bk == 0) ? 1 : 0;
   a.ksplit = pl.ksplit;
   a.partial = static_cast<float*>(q->workspace);
-  a.gn_part = reinterpret_cast<float2*>(q->gn_partial);
+  a.gn_part = reinterpret_cast<double*>(q->gn_partial);
+  a.gn_unit = q->gn_unit > 0 ? q->gn_unit : 1;
+  a.gn_slots = q->gn_slots > 0 ? q->gn_slots : 1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (use_halo) return launch_halo(a, s);
   if (pl.bm == 256) return launch_big(a, s);

@@ -1,10 +1,15 @@
 // GroupNorm(+SiLU) and LayerNorm over NHWC rows (ldm_group_norm / ldm_layer_norm).
 //
-// GroupNorm is HBM-bound.  Statistics come as per-channel (sum, sumsq) partials over 64-pixel
-// chunks — normally written by the producing conv's epilogue (ldm_conv2d gn_partial), so the
-// tensor is NOT re-read for them; otherwise gn_partial computes them here.
-//   gn_finalize: per (batch, group) fp64 reduction -> per-(batch, channel) scale/shift table
-//   gn_apply   : y = silu?(x * scale + shift), one 16-B vector per thread, one read + one write
+// GroupNorm is HBM-bound: one read and one write of the tensor, in ONE launch.  Its statistics
+// arrive as fp64 (sum, sumsq) accumulators per (batch, unit of U consecutive channels), summed
+// by the producing conv's epilogue (ldm_conv2d gn_partial / gn_unit), so the tensor is not
+// re-read for them (gn_stats computes them, U = 1, when no producer did).  Units, not groups:
+// one tensor feeds GroupNorms of different groupings (a skip is normalised alone in the down
+// path and at an offset inside an up-block concat) and U = 10 divides all of them.
+//   gn_apply  grid (row blocks, batch); issues its first UNR rows of loads, then reduces its
+//             batch's <= C / U accumulators to per-group (mean, rstd) in LDS while they are in
+//             flight (no separate finalize launch); every thread owns fixed 16-B channel columns,
+//             so its scale / shift live in registers, and streams y = silu?(x * scale + shift).
 // Inputs may be the channel concatenation of two NHWC tensors (up-block [hidden || skip]),
 // read in place.
 #include "common.h"
@@ -13,138 +18,163 @@
 
 namespace {
 
-constexpr int GN_PPC = 64;  // pixels per partial chunk (== the conv epilogue's 64-row chunks)
+constexpr int GN_MAXC = 2560;        // channels per GroupNorm (the UNet's largest concat)
+constexpr int GN_STATS_SLOTS = 4;    // accumulator copies written by the fallback statistics kernel
 
+// fallback statistics (no producer accumulators): grid (row blocks, batch); a block sums its
+// rows for every channel (column passes of <= 256 vectors, RB rows in parallel, fp32 over the
+// block's <= rows_per_block rows) and adds them to slot blockIdx.x % slots of the zeroed fp64
+// accumulators [batch][slots][C][2] (unit 1).
 template <typename T>
-__global__ __launch_bounds__(256) void gn_partial(const T* __restrict__ x, int C, int hw, int chunks,
-                                                  float2* __restrict__ part) {
+__global__ __launch_bounds__(256) void gn_stats(const T* __restrict__ x, int C, int hw, int rows_per_block,
+                                                int slots, double* __restrict__ acc) {
   constexpr int EPC = 16 / sizeof(T);
+  __shared__ float red[256 * EPC * 2];
   const int V = C / EPC;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int v = blockIdx.x * 64 + tx;
-  const int chunk = blockIdx.y, b = blockIdx.z;
-  float s[EPC], ss[EPC];
+  const int b = blockIdx.y;
+  const int r_beg = blockIdx.x * rows_per_block, r_end = min(hw, r_beg + rows_per_block);
+  double* dst = acc + ((int64_t)b * slots + blockIdx.x % slots) * C * 2;
+  for (int v0 = 0; v0 < V; v0 += 256) {
+    const int vn = min(256, V - v0);
+    const int rb = 256 / vn;
+    const int tx = threadIdx.x % vn, ty = threadIdx.x / vn;
+    float sm[EPC], sq[EPC];
 #pragma unroll
-  for (int e = 0; e < EPC; ++e) { s[e] = 0.f; ss[e] = 0.f; }
-  if (v < V) {
-    const int p0 = chunk * GN_PPC, p1 = min(hw, p0 + GN_PPC);
-    for (int pix = p0 + ty; pix < p1; pix += 4) {
-      const uint4 raw = *reinterpret_cast<const uint4*>(x + ((int64_t)b * hw + pix) * C + v * EPC);
-      const T* e = reinterpret_cast<const T*>(&raw);
+    for (int k = 0; k < EPC; ++k) { sm[k] = 0.f; sq[k] = 0.f; }
+    if (ty < rb)
+      for (int r = r_beg + ty; r < r_end; r += rb) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(x + ((int64_t)b * hw + r) * C + (v0 + tx) * EPC);
+        const T* e = reinterpret_cast<const T*>(&raw);
 #pragma unroll
-      for (int k = 0; k < EPC; ++k) {
-        const float f = to_f(e[k]);
-        s[k] += f;
-        ss[k] += f * f;
+        for (int k = 0; k < EPC; ++k) {
+          const float f = to_f(e[k]);
+          sm[k] += f;
+          sq[k] += f * f;
+        }
       }
-    }
-  }
-  __shared__ float red[4][64][EPC][2];
-#pragma unroll
-  for (int k = 0; k < EPC; ++k) { red[ty][tx][k][0] = s[k]; red[ty][tx][k][1] = ss[k]; }
-  __syncthreads();
-  if (ty == 0 && v < V) {
+    __syncthreads();                                   // the previous pass's reads of red are done
 #pragma unroll
     for (int k = 0; k < EPC; ++k) {
+      red[(threadIdx.x * EPC + k) * 2] = sm[k];
+      red[(threadIdx.x * EPC + k) * 2 + 1] = sq[k];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < vn * EPC; e += 256) {
+      const int col = e / EPC, k = e % EPC;
       float a = 0.f, q = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { a += red[j][tx][k][0]; q += red[j][tx][k][1]; }
-      part[((int64_t)b * chunks + chunk) * C + v * EPC + k] = make_float2(a, q);
-    }
-  }
-}
-
-// one 256-thread block per (batch, group): fp64 sum of the partials (each thread's loads are
-// unrolled 4-wide so they are in flight together — the partials are L2-resident, so this is a
-// latency problem, not a bandwidth one), then the group's scale/shift entries
-__global__ __launch_bounds__(256) void gn_finalize(const float2* __restrict__ part0, const float2* __restrict__ part1,
-                                                   int c0, int c1, int hw, int chunks, int groups, float eps,
-                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                   float2* __restrict__ table, float2* __restrict__ save) {
-  const int b = blockIdx.x;
-  const int gi = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int C = c0 + c1, cpg = C / groups;
-  const int n = chunks * cpg;
-  double a = 0.0, q = 0.0;
-  for (int i0 = tid; i0 < n; i0 += 4 * 256) {
-    float2 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = i0 + u * 256;
-      v[u] = make_float2(0.f, 0.f);
-      if (i < n) {
-        const int ch = i / cpg, c = gi * cpg + (i - ch * cpg);
-        const int64_t row = (int64_t)b * chunks + ch;
-        v[u] = c < c0 ? part0[row * c0 + c] : part1[row * c1 + (c - c0)];
+      for (int j = 0; j < rb; ++j) {
+        a += red[((j * vn + col) * EPC + k) * 2];
+        q += red[((j * vn + col) * EPC + k) * 2 + 1];
       }
+      double* d = dst + (int64_t)((v0 + col) * EPC + k) * 2;
+      unsafeAtomicAdd(d, (double)a);
+      unsafeAtomicAdd(d + 1, (double)q);
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) { a += v[u].x; q += v[u].y; }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { a += __shfl_xor(a, o, 64); q += __shfl_xor(q, o, 64); }
-  __shared__ double red[4][2];
-  if (lane == 0) { red[wave][0] = a; red[wave][1] = q; }
-  __syncthreads();
-  a = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-  q = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-  const double cnt = (double)hw * cpg;
-  const double mean = a / cnt;
-  double var = q / cnt - mean * mean;
-  if (var < 0.0) var = 0.0;
-  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
-  if (save && tid == 0) save[(int64_t)b * groups + gi] = make_float2((float)mean, rstd);   // for the backward
-  for (int k = tid; k < cpg; k += 256) {
-    const int c = gi * cpg + k;
-    const float sc = rstd * gamma[c];
-    table[(int64_t)b * C + c] = make_float2(sc, beta[c] - (float)mean * sc);
   }
 }
 
-// y = silu?(x * scale[b, c] + shift[b, c]) over 16-byte vectors; each thread takes UNR
-// vectors a grid-stride apart and issues all their loads before any math (HBM latency
-// overlaps), with 32-bit index math (nvec < 2^31 is checked on the host).
-template <typename T>
+// y = silu?(x * scale + shift).  Block = BX x RB threads: tx owns vector columns tx + BX * k
+// (k < NCOL) for all its rows, ty strides rows by RB; grid (row blocks, batch).  Dynamic LDS:
+// the batch's slots x C / unit accumulators (double2 each, <= 40 KB).
+template <typename T, int NCOL>
 __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x0, const T* __restrict__ x1, int c0, int c1,
-                                                int hw, int nvec, const float2* __restrict__ table, int act,
-                                                T* __restrict__ out) {
+                                                int hw, int rows_per_block, const double* __restrict__ acc0,
+                                                const double* __restrict__ acc1, int unit, int slots, int groups,
+                                                float eps,
+                                                const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                int act, T* __restrict__ out, float2* __restrict__ save) {
   constexpr int EPC = 16 / sizeof(T);
-  constexpr int UNR = 4;
-  const int C = c0 + c1, V = C / EPC;
-  const int step = gridDim.x * 256;
-  for (int i0 = blockIdx.x * 256 + threadIdx.x; i0 < nvec; i0 += UNR * step) {
-    uint4 raw[UNR];
-    int mm[UNR], cc[UNR];
+  constexpr int UNR = 8;
+  extern __shared__ double2 ured[];
+  __shared__ float2 gst[64];
+  const int C = c0 + c1, V = C / EPC, cpg = C / groups;
+  const int BX = blockDim.x, RB = blockDim.y;
+  const int tx = threadIdx.x, ty = threadIdx.y;
+  const int tid = ty * BX + tx, nt = BX * RB;
+  const int b = blockIdx.y;
+  const int r_beg = blockIdx.x * rows_per_block;
+  const int r_end = min(hw, r_beg + rows_per_block);
+  const int64_t rowb = (int64_t)b * hw;
+  const T* src[NCOL];
+  int ld[NCOL], cc[NCOL];
+  bool on[NCOL];
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int i = i0 + u * step;
-      const int m = i / V;
-      const int c = (i - m * V) * EPC;
-      mm[u] = m;
-      cc[u] = c;
-      if (i < nvec)
-        raw[u] = (c < c0) ? *reinterpret_cast<const uint4*>(x0 + (int64_t)m * c0 + c)
-                          : *reinterpret_cast<const uint4*>(x1 + (int64_t)m * c1 + (c - c0));
-    }
+  for (int k = 0; k < NCOL; ++k) {
+    const int v = tx + BX * k;
+    on[k] = v < V;
+    const int c = min(v, V - 1) * EPC;
+    cc[k] = c;
+    src[k] = c < c0 ? x0 + c : x1 + (c - c0);
+    ld[k] = c < c0 ? c0 : c1;
+  }
+  uint4 raw[NCOL][UNR];
+  auto load = [&](int r0) {
 #pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      if (i0 + u * step >= nvec) break;
-      const int b = mm[u] / hw, c = cc[u];
-      const T* e = reinterpret_cast<const T*>(&raw[u]);
-      const float4* tb = reinterpret_cast<const float4*>(table + (int64_t)b * C + c);
-      uint4 res;
-      T* r = reinterpret_cast<T*>(&res);
+    for (int k = 0; k < NCOL; ++k)
 #pragma unroll
-      for (int k = 0; k < EPC; k += 2) {
-        const float4 st = tb[k >> 1];   // (scale_k, shift_k, scale_k+1, shift_k+1)
-        float y0 = to_f(e[k]) * st.x + st.y;
-        float y1 = to_f(e[k + 1]) * st.z + st.w;
-        if (act == LDM_ACT_SILU) { y0 = silu_f(y0); y1 = silu_f(y1); }
-        r[k] = from_f<T>(y0);
-        r[k + 1] = from_f<T>(y1);
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * RB;
+        if (on[k] && r < r_end) raw[k][u] = *reinterpret_cast<const uint4*>(src[k] + (rowb + r) * ld[k]);
       }
-      *reinterpret_cast<uint4*>(out + (int64_t)mm[u] * C + c) = res;
+  };
+  load(r_beg + ty);                 // the first pass's rows are in flight during the statistics
+  // accumulators -> LDS (all loads in flight), then thread per group: mean / rstd in fp64
+  const int u0 = c0 / unit, u1 = c1 / unit, upg = cpg / unit;
+  const int un = u0 + u1;
+  for (int i = tid; i < slots * un; i += nt) {              // entry (slot, unit): all loads in flight
+    const int sl = i / un, u = i - sl * un;
+    ured[i] = u < u0 ? *reinterpret_cast<const double2*>(acc0 + (((int64_t)b * slots + sl) * u0 + u) * 2)
+                     : *reinterpret_cast<const double2*>(acc1 + (((int64_t)b * slots + sl) * u1 + (u - u0)) * 2);
+  }
+  __syncthreads();
+  for (int gi = tid; gi < groups; gi += nt) {
+    double sa = 0.0, sq = 0.0;
+    for (int sl = 0; sl < slots; ++sl)
+      for (int k = 0; k < upg; ++k) {
+        const double2 v = ured[sl * un + gi * upg + k];
+        sa += v.x;
+        sq += v.y;
+      }
+    const double cnt = (double)hw * cpg;
+    const double mean = sa / cnt;
+    double var = sq / cnt - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float2 ms = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)eps)));
+    gst[gi] = ms;
+    if (save && blockIdx.x == 0) save[b * groups + gi] = ms;   // training: kept for the backward
+  }
+  __syncthreads();
+  float sc[NCOL][EPC], sh[NCOL][EPC];
+#pragma unroll
+  for (int k = 0; k < NCOL; ++k) {
+#pragma unroll
+    for (int e = 0; e < EPC; ++e) {
+      const int c = cc[k] + e;
+      const float2 ms = gst[c / cpg];
+      sc[k][e] = ms.y * gamma[c];
+      sh[k][e] = beta[c] - ms.x * sc[k][e];
+    }
+  }
+  for (int r0 = r_beg + ty; r0 < r_end; r0 += UNR * RB) {
+    if (r0 != r_beg + ty) load(r0);
+#pragma unroll
+    for (int k = 0; k < NCOL; ++k) {
+      if (!on[k]) continue;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const int r = r0 + u * RB;
+        if (r >= r_end) break;
+        const T* e = reinterpret_cast<const T*>(&raw[k][u]);
+        uint4 res;
+        T* o = reinterpret_cast<T*>(&res);
+#pragma unroll
+        for (int j = 0; j < EPC; ++j) {
+          float y = to_f(e[j]) * sc[k][j] + sh[k][j];
+          if (act == LDM_ACT_SILU) y = silu_f(y);
+          o[j] = from_f<T>(y);
+        }
+        *reinterpret_cast<uint4*>(out + (rowb + r) * C + cc[k]) = res;
+      }
     }
   }
 }
@@ -257,39 +287,48 @@ inline size_t round16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 template <typename T>
 int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups, const float* gamma,
-              const float* beta, float eps, int act, void* out, const float* p0, const float* p1, void* ws,
-              float* save, hipStream_t s) {
+              const float* beta, float eps, int act, void* out, const double* a0, const double* a1, int unit,
+              int slots, void* ws, float* save, hipStream_t s) {
   constexpr int EPC = 16 / sizeof(T);
-  const int C = c0 + c1;
-  const int chunks = (hw + GN_PPC - 1) / GN_PPC;
-  char* w = static_cast<char*>(ws);
-  float2* table = reinterpret_cast<float2*>(w);
-  w += round16((size_t)batch * C * sizeof(float2));
-  const float2* part0 = reinterpret_cast<const float2*>(p0);
-  const float2* part1 = reinterpret_cast<const float2*>(p1);
-  if (!part0) {
-    float2* dst = reinterpret_cast<float2*>(w);
-    w += round16((size_t)batch * chunks * c0 * sizeof(float2));
-    hipLaunchKernelGGL((gn_partial<T>), dim3((c0 / EPC + 63) / 64, chunks, batch), dim3(256), 0, s,
-                       static_cast<const T*>(x0), c0, hw, chunks, dst);
+  const int C = c0 + c1, V = C / EPC;
+  if ((a0 && !a1 && c1 > 0) || (!a0 && a1)) a0 = a1 = nullptr;     // one layout for both: recompute both
+  if (!a0) {
+    unit = 1;
+    slots = std::max(1, std::min(GN_STATS_SLOTS, GN_MAXC / C));    // slots x C entries fit the LDS
+    double* w = static_cast<double*>(ws);
+    if (hipMemsetAsync(w, 0, (size_t)batch * slots * C * 2 * sizeof(double), s) != hipSuccess) return LDM_ERR_LAUNCH;
+    const int rpb = std::max(64, (int)(((int64_t)hw * batch + 1023) / 1024));
+    const dim3 grid((hw + rpb - 1) / rpb, batch);
+    hipLaunchKernelGGL((gn_stats<T>), grid, dim3(256), 0, s, static_cast<const T*>(x0), c0, hw, rpb, slots, w);
     LDM_CHECK_LAUNCH();
-    part0 = dst;
+    a0 = w;
+    if (c1 > 0) {
+      w += (size_t)batch * slots * c0 * 2;
+      hipLaunchKernelGGL((gn_stats<T>), grid, dim3(256), 0, s, static_cast<const T*>(x1), c1, hw, rpb, slots, w);
+      LDM_CHECK_LAUNCH();
+      a1 = w;
+    }
   }
-  if (c1 > 0 && !part1) {
-    float2* dst = reinterpret_cast<float2*>(w);
-    hipLaunchKernelGGL((gn_partial<T>), dim3((c1 / EPC + 63) / 64, chunks, batch), dim3(256), 0, s,
-                       static_cast<const T*>(x1), c1, hw, chunks, dst);
-    LDM_CHECK_LAUNCH();
-    part1 = dst;
-  }
-  hipLaunchKernelGGL(gn_finalize, dim3(batch, groups), dim3(256), 0, s, part0, part1, c0, c1, hw, chunks,
-                     groups, eps, gamma, beta, table, reinterpret_cast<float2*>(save));
-  LDM_CHECK_LAUNCH();
-  const int64_t nvec = (int64_t)batch * hw * (C / EPC);
-  if (nvec >= (1LL << 31) - 4 * 256 * 2048) return LDM_ERR_ARG;
-  const int64_t blocks = std::min<int64_t>((nvec + 4 * 256 - 1) / (4 * 256), 256 * 8);
-  hipLaunchKernelGGL((gn_apply<T>), dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const T*>(x0),
-                     static_cast<const T*>(x1), c0, c1, hw, (int)nvec, table, act, static_cast<T*>(out));
+  // columns: NCOL per thread so BX <= 256; rows: RB per pass, ~1024 blocks in all (one pass of
+  // UNR rows per thread at the 64x64 / 32x32 levels: every load in flight at once)
+  const int ncol = (V + 255) / 256;
+  const int bx = (V + ncol - 1) / ncol;
+  const int rb = std::max(1, 256 / bx);
+  const int per_b = std::max(1, std::min((hw + rb - 1) / rb, (1024 + batch - 1) / batch));
+  const int rpb = (hw + per_b - 1) / per_b;
+  const int nb = (hw + rpb - 1) / rpb;
+  const dim3 grid(nb, batch), block(bx, rb);
+  const size_t lds = (size_t)slots * (C / unit) * sizeof(double2);
+  if (lds > GN_MAXC * sizeof(double2)) return LDM_ERR_ARG;
+#define GN_APPLY(NC)                                                                                        \
+  hipLaunchKernelGGL((gn_apply<T, NC>), grid, block, lds, s, static_cast<const T*>(x0),                     \
+                     static_cast<const T*>(x1), c0, c1, hw, rpb, a0, a1, unit, slots, groups, eps, gamma, beta, \
+                     act, static_cast<T*>(out), reinterpret_cast<float2*>(save))
+  if (ncol == 1) GN_APPLY(1);
+  else if (ncol == 2) GN_APPLY(2);
+  else if (ncol == 3) GN_APPLY(3);
+  else return LDM_ERR_ARG;
+#undef GN_APPLY
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
@@ -297,38 +336,39 @@ int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw,
 }  // namespace
 
 extern "C" size_t ldm_group_norm_workspace_bytes(int batch, int hw, int channels) {
-  const size_t chunks = (hw + GN_PPC - 1) / GN_PPC;
-  return round16((size_t)batch * channels * sizeof(float2)) + 2 * round16((size_t)batch * chunks * channels *
-                                                                          sizeof(float2)) + 64;
+  (void)hw;
+  return round16((size_t)batch * GN_STATS_SLOTS * channels * 2 * sizeof(double)) + 64;   // fallback accumulators
 }
 
 extern "C" int ldm_group_norm_ex(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
                                  const float* gamma, const float* beta, float eps, int act, void* out,
-                                 const float* stats0, const float* stats1, void* workspace, float* save_mean_rstd,
-                                 int dtype, ldm_stream_t stream) {
+                                 const double* stats0, const double* stats1, int stats_unit, int stats_slots,
+                                 void* workspace, float* save_mean_rstd, int dtype, ldm_stream_t stream) {
   if (!x0 || !out || !workspace || !gamma || !beta) return LDM_ERR_ARG;
   if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
-  if (batch <= 0 || hw <= 0 || c0 <= 0 || c1 < 0 || (c1 > 0 && !x1) || groups <= 0) return LDM_ERR_ARG;
+  if (batch <= 0 || hw <= 0 || c0 <= 0 || c1 < 0 || (c1 > 0 && !x1) || groups <= 0 || groups > 64) return LDM_ERR_ARG;
   const int C = c0 + c1;
-  if (C % groups) return LDM_ERR_ARG;
-  if ((stats0 || stats1) && hw % GN_PPC) return LDM_ERR_ARG;   // producer partials use 64-row chunks
+  if (C % groups || C > GN_MAXC) return LDM_ERR_ARG;
+  if ((stats0 || stats1) && (stats_unit <= 0 || stats_slots <= 0 || c0 % stats_unit || c1 % stats_unit ||
+                             (C / groups) % stats_unit))
+    return LDM_ERR_ARG;
   const int epc = dtype == LDM_F32 ? 4 : 8;
   if (c0 % epc || c1 % epc) return LDM_ERR_ALIGN;
   if (!aligned16(x0) || (x1 && !aligned16(x1)) || !aligned16(out) || !aligned16(workspace)) return LDM_ERR_ALIGN;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (dtype == LDM_BF16)
     return gn_launch<bf16_t>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1,
-                             workspace, save_mean_rstd, s);
-  return gn_launch<float>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1, workspace,
-                          save_mean_rstd, s);
+                             stats_unit, stats_slots, workspace, save_mean_rstd, s);
+  return gn_launch<float>(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1, stats_unit,
+                          stats_slots, workspace, save_mean_rstd, s);
 }
 
 extern "C" int ldm_group_norm(const void* x0, const void* x1, int c0, int c1, int batch, int hw, int groups,
                               const float* gamma, const float* beta, float eps, int act, void* out,
-                              const float* stats0, const float* stats1, void* workspace, int dtype,
-                              ldm_stream_t stream) {
-  return ldm_group_norm_ex(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1, workspace,
-                           nullptr, dtype, stream);
+                              const double* stats0, const double* stats1, int stats_unit, int stats_slots,
+                              void* workspace, int dtype, ldm_stream_t stream) {
+  return ldm_group_norm_ex(x0, x1, c0, c1, batch, hw, groups, gamma, beta, eps, act, out, stats0, stats1, stats_unit,
+                           stats_slots, workspace, nullptr, dtype, stream);
 }
 
 extern "C" int ldm_layer_norm(const void* x, int rows, int c, const float* gamma, const float* beta, float eps,

@@ -209,6 +209,10 @@ class GeneralVAEImage(nn.Module):
     @torch.no_grad()
     def encode_moments(self, x):
         """x [B, 3, H, W] in [-1, 1] -> moments fp32 [B, 2L, H/8, W/8] (encoder + quant_conv)."""
+        with K.gn_arena(("vae_image", id(self), tuple(x.shape), self.dtype), x.device):
+            return self._encode_moments(x)
+
+    def _encode_moments(self, x):
         P = self.prepare()
         B, _, H, W = x.shape
         if H % 8 or W % 8:

@@ -551,7 +551,13 @@ class UNet(nn.Module):
     def forward_sources(self, sources, timestep, encoder_hidden_states=None):
         """forward() on the channel concatenation of up to three NCHW tensors without
         materialising it (the sampler's ``torch.cat([x_t, rgb, cond], 1)``,
-        trainers_ldm_cond.py:1134-1141, is folded into the NCHW->NHWC gather of conv_in)."""
+        trainers_ldm_cond.py:1134-1141, is folded into the NCHW->NHWC gather of conv_in).
+        All GroupNorm accumulators of the pass come from one zeroed arena (K.gn_arena)."""
+        s0 = sources[0]
+        with K.gn_arena(("unet", id(self), tuple(s0.shape), self.compute_dtype), s0.device):
+            return self._forward_sources(sources, timestep, encoder_hidden_states)
+
+    def _forward_sources(self, sources, timestep, encoder_hidden_states=None):
         P = self.prepare()
         dt = self.compute_dtype
         sample = sources[0]

@@ -141,6 +141,11 @@ class UNetTrainGraph:
         return out
 
     def forward(self, sources, timestep):
+        s0 = sources[0]
+        with K.gn_arena(("unet_train", id(self.u), tuple(s0.shape), self.u.compute_dtype), s0.device):
+            return self._forward(sources, timestep)
+
+    def _forward(self, sources, timestep):
         u, P = self.u, self.P
         if any(p.requires_grad for p in u.time_embedding.parameters()):
             raise NotImplementedError("a trainable time_embedding is not supported on the native training path "

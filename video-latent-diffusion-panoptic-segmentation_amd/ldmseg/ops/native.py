@@ -5,6 +5,7 @@ no fallback: if the library is missing, or a tensor is not on the GPU, the call 
 Host-side checks (device, dtype, contiguity, shapes) run before any launch so that a bad
 call can never reach the GPU as an out-of-bounds kernel.
 """
+import contextlib
 import ctypes
 import math
 import os
@@ -33,7 +34,7 @@ class ConvParams(ctypes.Structure):
                 ("h_out", _i), ("w_out", _i), ("ksize", _i), ("stride", _i), ("upsample", _i), ("w", _vp),
                 ("n", _i), ("kpad", _i), ("bias", _vp), ("temb", _vp), ("temb_stride", _i), ("residual", _vp),
                 ("out", _vp), ("out_layout", _i), ("act", _i), ("dtype", _i), ("out_f32", _i),
-                ("workspace", _vp), ("workspace_bytes", _i64), ("gn_partial", _vp), ("pad_mode", _i)]
+                ("workspace", _vp), ("workspace_bytes", _i64), ("gn_partial", _vp), ("pad_mode", _i), ("gn_unit", _i), ("gn_slots", _i)]
 
 
 class AttnParams(ctypes.Structure):
@@ -66,7 +67,7 @@ EXPORTS = {
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_group_norm_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
-    "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _i, _vp]),
+    "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _i, _i, _vp, _i, _vp]),
     "ldm_layer_norm": (_i, [_vp, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp]),
     "ldm_timestep_proj": (_i, [_vp, _i, _i, _vp, _i, _i, _vp, _i, _vp]),
     "ldm_ddim_step": (_i, [ctypes.POINTER(DdimParams), _vp]),
@@ -82,7 +83,8 @@ EXPORTS = {
     "ldm_attention_set_waves": (None, [_i]),
     "ldm_attention_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_bwd": (_i, [ctypes.POINTER(AttnParams), _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
-    "ldm_group_norm_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    "ldm_group_norm_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _i, _i, _vp, _vp,
+                               _i, _vp]),
     "ldm_conv2d_wgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(WgradParams)]),
     "ldm_conv2d_wgrad": (_i, [ctypes.POINTER(WgradParams), _vp]),
     "ldm_colsum": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp]),
@@ -306,16 +308,71 @@ GN_PART_ATTR = "_ldm_gn_part"
 
 
 def gn_stats_of(t):
-    """The (sum, sumsq) partial slab a conv epilogue attached to tensor ``t`` (or None)."""
+    """The fp64 [batch, slots, c / unit, 2] (sum, sumsq) accumulators a conv epilogue attached to
+    ``t`` (or None); unit = channels per accumulator, slots = copies the row tiles spread over."""
     return getattr(t, GN_PART_ATTR, None) if t is not None else None
+
+
+GN_UNIT_MAX = 10          # tuning hook (A/B only): 1 = one accumulator per channel
+
+
+def gn_unit_for(n):
+    """Channels per GroupNorm accumulator of an n-channel conv output: 10 for the SD UNet widths
+    (it divides every group size, 10..80, and every concat offset), else gcd(n, 10)."""
+    return math.gcd(n, GN_UNIT_MAX)
+
+
+def gn_slots_for(hw):
+    """Accumulator copies for an output of hw pixels per image: same-address fp64 atomics
+    serialise, so the ~hw/128 row tiles of one image are spread over up to 8 copies."""
+    return max(1, min(8, hw // 256))
+
+
+_gn_arena_tls = threading.local()
+_gn_arena_sizes = {}
+
+
+@contextlib.contextmanager
+def gn_arena(key, device):
+    """Scope (one forward) in which conv2d(gn_stats=True) takes its zeroed GroupNorm accumulators
+    as slices of ONE zero-filled fp64 buffer — one memset per forward instead of one per conv.
+    The buffer is sized from the previous forward with the same ``key`` (the first one falls back
+    to a torch.zeros per conv and records how much it needed)."""
+    need = _gn_arena_sizes.get(key, 0)
+    st = {"buf": torch.zeros(need, dtype=torch.float64, device=device) if need else None, "off": 0, "used": 0}
+    stack = getattr(_gn_arena_tls, "stack", None)
+    if stack is None:
+        stack = _gn_arena_tls.stack = []
+    stack.append(st)
+    try:
+        yield
+    finally:
+        stack.pop()
+        _gn_arena_sizes[key] = max(need, st["used"])
+
+
+def _gn_accumulators(batch, slots, n, device):
+    """Zeroed fp64 [batch, slots, n, 2] accumulators (n = units), from the enclosing gn_arena if any."""
+    cnt = batch * slots * n * 2                   # even -> every slice stays 16-B aligned
+    stack = getattr(_gn_arena_tls, "stack", None)
+    if stack:
+        st = stack[-1]
+        st["used"] += cnt
+        buf = st["buf"]
+        if buf is not None and buf.device == device and st["off"] + cnt <= buf.numel():
+            v = buf[st["off"]:st["off"] + cnt].view(batch, slots, n, 2)
+            st["off"] += cnt
+            return v
+    return torch.zeros(batch, slots, n, 2, dtype=torch.float64, device=device)
 
 
 def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False, temb=None, temb_stride=0,
            residual=None, out=None, out_layout=OUT_NHWC, act=ACT_NONE, out_dtype=None, gn_stats=False, pad_mode=0):
     """Run ldm_conv2d.  x0/x1: NHWC [batch, h, w, c] (any contiguous view with that numel).
 
-    gn_stats=True also has the epilogue write per-64-row-chunk channel (sum, sumsq) of the
-    output; the slab is attached to the returned tensor and consumed by group_norm()."""
+    gn_stats=True also has the epilogue sum the per-(batch, channel) (sum, sumsq) of the output
+    into fp64 accumulators (from the enclosing gn_arena when there is one); they are attached to
+    the returned tensor and consumed by group_norm()."""
     lib = load_library()
     _gpu(x0, x1, pc.w, temb, residual, out)
     c0 = x0.numel() // (batch * h * w)
@@ -361,13 +418,14 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
         if temb.shape[1] < n or temb.stride(0) != temb_stride:
             raise ValueError("temb view narrower than n or stride mismatch")
     M = batch * ho * wo
-    part = None
+    part, unit, slots = None, 0, 0
     if gn_stats and out_layout == OUT_NHWC and M % 64 == 0 and (ho * wo) % 64 == 0:
-        part = torch.empty(M // 64, n, 2, dtype=torch.float32, device=x0.device)
+        unit, slots = gn_unit_for(n), gn_slots_for(ho * wo)
+        part = _gn_accumulators(batch, slots, n // unit, x0.device)
     p = ConvParams(_ptr(x0), _ptr(x1), c0, c1, batch, h, w, ho, wo, pc.ksize, stride, int(upsample), _ptr(pc.w),
                    n, pc.kpad, _ptr(pc.bias), _ptr(temb), temb_stride, _ptr(residual), _ptr(out), out_layout, act,
                    dtype_code(pc.dtype), int(odt == torch.float32 and pc.dtype != torch.float32), None, 0,
-                   _ptr(part), int(pad_mode))
+                   _ptr(part), int(pad_mode), unit, slots)
     ws_bytes = int(lib.ldm_conv2d_workspace_bytes(ctypes.byref(p)))
     if ws_bytes:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x0.device)
@@ -473,6 +531,29 @@ def attention(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_
     return out
 
 
+def _gn_checked(x, batch, c):
+    s = gn_stats_of(x)
+    if s is not None and (s.dtype != torch.float64 or s.ndim != 4 or s.shape[0] != batch or s.shape[3] != 2
+                          or s.shape[2] == 0 or c % s.shape[2] or not s.is_contiguous()):
+        raise ValueError("attached GroupNorm accumulators do not match the tensor")
+    return s
+
+
+def _gn_sources(x0, x1, batch, c0, c1, groups):
+    """(stats0, stats1, unit, slots) the kernel can consume, or (None, None, 0, 0): one unit and
+    slot count for both sources, the unit dividing the group size and the concat offset (else the
+    kernel recomputes the statistics)."""
+    s0, s1 = _gn_checked(x0, batch, c0), _gn_checked(x1, batch, c1)
+    if s0 is None or (c1 and s1 is None):
+        return None, None, 0, 0
+    unit, slots = c0 // s0.shape[2], s0.shape[1]
+    if c1 and (c1 // s1.shape[2] != unit or s1.shape[1] != slots):
+        return None, None, 0, 0
+    if (c0 + c1) % groups or ((c0 + c1) // groups) % unit or slots * (c0 + c1) // unit > 2560:
+        return None, None, 0, 0                   # (the kernel stages slots x units in <= 40 KB of LDS)
+    return s0, s1, unit, slots
+
+
 def group_norm(x0, batch, hw, groups, gamma, beta, eps, act=ACT_NONE, x1=None, out=None):
     """GroupNorm over NHWC [batch, hw, c0 (+c1)] -> contiguous NHWC [batch, hw, c0+c1]."""
     lib = load_library()
@@ -487,17 +568,12 @@ def group_norm(x0, batch, hw, groups, gamma, beta, eps, act=ACT_NONE, x1=None, o
     if out is None:
         out = torch.empty(batch, hw, C, dtype=x0.dtype, device=x0.device)
     ws = torch.empty(int(lib.ldm_group_norm_workspace_bytes(batch, hw, C)), dtype=torch.uint8, device=x0.device)
-    s0, s1 = gn_stats_of(x0), gn_stats_of(x1)
-    if hw % 64:
-        s0 = s1 = None
-    for s, c in ((s0, c0), (s1, c1)):
-        if s is not None and s.numel() != (batch * hw // 64) * c * 2:
-            raise ValueError("attached GroupNorm partials do not match the tensor")
+    s0, s1, unit, slots = _gn_sources(x0, x1, batch, c0, c1, groups)
     ev = _prof_start()
     _check(lib.ldm_group_norm(_ptr(x0), _ptr(x1), c0, c1, batch, hw, groups, _ptr(gamma), _ptr(beta), float(eps),
-                              act, _ptr(out), _ptr(s0), _ptr(s1), _ptr(ws), dtype_code(x0.dtype), _stream(x0)),
-           "ldm_group_norm")
-    passes = 2.0 + (s0 is None) * c0 / C + (x1 is not None and s1 is None) * c1 / C
+                              act, _ptr(out), _ptr(s0), _ptr(s1), unit, slots, _ptr(ws), dtype_code(x0.dtype),
+                              _stream(x0)), "ldm_group_norm")
+    passes = 2.0 + (s0 is None) * 1.0
     _prof_stop(ev, "group_norm", 0.0, passes * out.numel() * out.element_size(),
                f"hw={hw} C={c0}+{c1} fused_stats={s0 is not None}")
     return out
@@ -786,12 +862,10 @@ def group_norm_train(x0, batch, hw, groups, gamma, beta, eps, act=ACT_NONE, x1=N
     out = torch.empty(batch, hw, C, dtype=x0.dtype, device=x0.device)
     mr = torch.empty(batch, groups, 2, dtype=torch.float32, device=x0.device)
     ws = torch.empty(int(lib.ldm_group_norm_workspace_bytes(batch, hw, C)), dtype=torch.uint8, device=x0.device)
-    s0, s1 = gn_stats_of(x0), gn_stats_of(x1)
-    if hw % 64:
-        s0 = s1 = None
+    s0, s1, unit, slots = _gn_sources(x0, x1, batch, c0, c1, groups)
     _check(lib.ldm_group_norm_ex(_ptr(x0), _ptr(x1), c0, c1, batch, hw, groups, _ptr(gamma), _ptr(beta), float(eps),
-                                 act, _ptr(out), _ptr(s0), _ptr(s1), _ptr(ws), _ptr(mr), dtype_code(x0.dtype),
-                                 _stream(x0)), "ldm_group_norm_ex")
+                                 act, _ptr(out), _ptr(s0), _ptr(s1), unit, slots, _ptr(ws), _ptr(mr),
+                                 dtype_code(x0.dtype), _stream(x0)), "ldm_group_norm_ex")
     return out, mr
 
 
