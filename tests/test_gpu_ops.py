@@ -216,6 +216,31 @@ def test_attention_softmax_spike():
     assert rel_err(o, ref) < 1e-4
 
 
+@pytest.mark.parametrize("maxcol", [True, False])
+@pytest.mark.parametrize("C,N", [(320, 520), (640, 300), (320, 4096)])
+def test_attention_softmax_spike_bf16(C, N, maxcol):
+    """bf16 kernel under forced rescales, with and without the max column (scale and running max
+    carried in the Q.K^T head-dim padding): a huge logit in the last kv tile, a first kv tile
+    whose logits are all very negative for some rows (the first-tile max must still be taken),
+    and a row whose max grows tile after tile."""
+    torch.manual_seed(14)
+    B = 1
+    q, k, v = torch.randn(B, N, C), torch.randn(B, N, C), torch.randn(B, N, C)
+    k[0, N - 3] = q[0, 7] * 4.0                      # spike in the last tile
+    k[0, :64] -= q[0, 11] * 3.0                      # row 11: first tile far below the rest
+    for t in range(1, N // 64):                      # row 5: max grows every tile
+        k[0, 64 * t + 1] = q[0, 5] * (0.5 * t / (N // 64))
+    ref = _attn_ref(q, k, v, 8)
+    qkv = torch.cat([q, k, v], -1).to(DEV, torch.bfloat16)
+    K.set_attention_maxcol(maxcol)
+    try:
+        o = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, 8, C // 8, N, N, 3 * C, 3 * C, 3 * C)
+    finally:
+        K.set_attention_maxcol(True)
+    assert rel_err(o, ref) < 2e-2
+    assert (o.float() - ref.to(DEV)).abs().max().item() < 0.05
+
+
 # ------------------------------------------------------------------------------ norms
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("B,HW,c0,c1,G,eps,act", [(2, 4096, 320, 0, 32, 1e-5, True), (2, 256, 1280, 1280, 32, 1e-5, True),

@@ -345,7 +345,25 @@ __device__ __forceinline__ uint32_t bf16x4_to_fp8x4(uint2 v) {
                     sat448(__uint_as_float(v.y << 16)), sat448(__uint_as_float(v.y & 0xffff0000u)));
 }
 
-template <int DP, int QSUB, bool ONES, int NW = 4, int OCC = 8 / NW, bool F8 = false>
+// MC ("max column", head_dim % 32 != 0 and % 8 == 0): the softmax's scale and running max ride
+// in the Q.K^T MFMA's head-dim padding instead of one FMA per score.  Q is prescaled by
+// scale * log2(e) (bf16), Q[:, d] = -m (m bf16-exact) and K[:, d] = 1, so the accumulator is
+// already s * c - m and p = exp2(acc).  When the max grows past the lazy-rescale threshold the
+// tile's accumulators are shifted once and the Q column rewritten; numerator and denominator
+// (ones column of V) see the same m, so its bf16 rounding cancels.
+__device__ __forceinline__ float bf16_rne(float x) {
+  const unsigned u = __float_as_uint(x);
+  return __uint_as_float((u + 0x7fffu + ((u >> 16) & 1u)) & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 scale_bf16x8(uint4 v, float c) {
+  unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = pack_bf16x2(__uint_as_float(w[i] << 16) * c, __uint_as_float(w[i] & 0xffff0000u) * c);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int DP, int QSUB, bool ONES, int NW = 4, int OCC = 8 / NW, bool F8 = false, bool MC = false>
 __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) {
   typedef bf16_t T;
   constexpr int ES = 2, EPC = 8;
@@ -392,7 +410,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
       const int row = L / RCH, c = L - row * RCH;
       const int kv = kv0 + row, d = c * EPC;
       const bool ok = kv < p.nkv && c < CPR && d < p.d;
-      const void* ks = ok ? (const void*)(kp + (int64_t)kv * p.ks + d) : (const void*)&kZeros16;
+      const bool kone = MC && c == p.d / EPC && kv < p.nkv;      // K[:, d] = 1 (max column)
+      const void* ks = ok ? (const void*)(kp + (int64_t)kv * p.ks + d)
+                          : (kone ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
       const void* vs = ok ? (const void*)(vp + (int64_t)kv * p.vs + d)
                           : (c == ones_chunk ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
       const unsigned off = __builtin_amdgcn_readfirstlane(i * 64 * 16);
@@ -400,8 +420,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
       glds16(vs, vb + off);
     }
   };
+  const float c2 = p.scale_log2;
 
-  // Q fragments: x32 chunk c: lane holds Q[q][32c + 8g .. +8] (zero past head_dim)
+  // Q fragments: x32 chunk c: lane holds Q[q][32c + 8g .. +8] (zero past head_dim; MC: * c2,
+  // and column d = -m, initially 0)
   Frag8<T> q32[QSUB][NC];
 #pragma unroll
   for (int s = 0; s < QSUB; ++s) {
@@ -410,10 +432,15 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int dd = 32 * c + 8 * g;
-      if (qi < p.nq && dd < p.d) q32[s][c].v = *reinterpret_cast<const uint4*>(qrow + dd);
-      else q32[s][c].v = make_uint4(0u, 0u, 0u, 0u);
+      if (qi < p.nq && dd < p.d) {
+        const uint4 raw = *reinterpret_cast<const uint4*>(qrow + dd);
+        q32[s][c].v = MC ? scale_bf16x8(raw, c2) : raw;
+      } else {
+        q32[s][c].v = make_uint4(0u, 0u, 0u, 0u);
+      }
     }
   }
+  const int gq = (p.d & 31) >> 3;                       // MC: lane group holding Q column d
 
   f32x4_t oacc[ND][QSUB];
 #pragma unroll
@@ -422,10 +449,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
     for (int s = 0; s < QSUB; ++s) oacc[i][s] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   float mrun[QSUB], lrun[QSUB];
 #pragma unroll
-  for (int s = 0; s < QSUB; ++s) { mrun[s] = -INFINITY; lrun[s] = 0.f; }
-  const float c2 = p.scale_log2;
+  for (int s = 0; s < QSUB; ++s) { mrun[s] = MC ? 0.f : -INFINITY; lrun[s] = 0.f; }
 
-  auto compute = [&](int buf, int kv0, bool masked) {
+  auto compute = [&](int buf, int kv0, bool masked, bool first) {
     const T* Ks = lds + buf * 2 * TILE;
     const T* Vs = Ks + TILE;
     f32x4_t sacc[4][QSUB];
@@ -470,6 +496,36 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
       float mx = vmax3(m0, m1, m2);
       mx = vmax3(mx, m3, m4);
       mx = max_over_groups_raw(vmax3(mx, sacc[3][s][3], sacc[3][s][3]));
+      if constexpr (MC) {
+        // accumulators are s * c2 - m already; the first tile always sets m (from m = 0)
+        if (first || __any(mx > kRescaleThr)) {
+          const float tgt = mrun[s] + mx;
+          const float mn = bf16_rne(first ? tgt : fmaxf(mrun[s], tgt));
+          const float delta = mn - mrun[s];
+          const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);   // (O = 0 on the first tile)
+          mrun[s] = mn;
+          if (!ONES) lrun[s] *= alpha;
+#pragma unroll
+          for (int i = 0; i < ND; ++i) oacc[i][s] *= alpha;
+#pragma unroll
+          for (int js = 0; js < 4; ++js) sacc[js][s] -= delta;
+          if (g == gq) q32[s][NC - 1].v.x = (q32[s][NC - 1].v.x & 0xffff0000u) | (__float_as_uint(-mn) >> 16);
+        }
+        float lsum = 0.f;
+#pragma unroll
+        for (int js = 0; js < 4; ++js) {
+          float pv[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            pv[r] = __builtin_amdgcn_exp2f(sacc[js][s][r]);
+            if (!ONES) lsum += pv[r];
+          }
+          if constexpr (F8) pk8[js][s] = pack_fp8x4(pv[0], pv[1], pv[2], pv[3]);
+          else pk[js][s] = make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
+        }
+        if (!ONES) lrun[s] += lsum;
+        continue;
+      }
       const float ms = mx * c2;
       if (__any(ms > mrun[s] + kRescaleThr)) {
         const float mnew = fmaxf(mrun[s], ms);
@@ -542,11 +598,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
   __syncthreads();
   for (int t = 0; t < nfull; ++t) {
     if (t + 1 < ntiles) issue_tile((t + 1) * KVT, (t + 1) & 1);
-    compute(t & 1, t * KVT, false);
+    compute(t & 1, t * KVT, false, t == 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (nfull < ntiles) compute(nfull & 1, nfull * KVT, true);
+  if (nfull < ntiles) compute(nfull & 1, nfull * KVT, true, nfull == 0);
 
   T* op = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * p.d;
 #pragma unroll
@@ -575,31 +631,33 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 
 int g_attn_waves = 0;   // 0: auto (8 when that still gives >= 256 blocks), 4 or 8: forced
 
-template <int DP, int QSUB, bool ONES, bool F8 = false>
+template <int DP, int QSUB, bool ONES, bool F8 = false, bool MC = false>
 int launch32_cfg(const AttnArgs& a, int batch, hipStream_t s) {
   const int blocks8 = (a.nq + 128 * QSUB - 1) / (128 * QSUB) * a.heads * batch;
   if (g_attn_waves == 8 || (g_attn_waves == 0 && blocks8 >= 256)) {
     // 8 waves share every K/V tile (one 512-thread block per CU): half the LDS-DMA bytes per FLOP
     const int nblk = (a.nq + 128 * QSUB - 1) / (128 * QSUB) * a.heads * batch;
-    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 8, 1, F8>), dim3(nblk), dim3(512), 0, s, a);
+    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 8, 1, F8, MC>), dim3(nblk), dim3(512), 0, s, a);
   } else {
     const int nblk = (a.nq + 64 * QSUB - 1) / (64 * QSUB) * a.heads * batch;
-    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 4, 2, F8>), dim3(nblk), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, 4, 2, F8, MC>), dim3(nblk), dim3(256), 0, s, a);
   }
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
 
-template <int DP, int QSUB, bool ONES, int NW, int OCC, bool F8 = false>
+template <int DP, int QSUB, bool ONES, int NW, int OCC, bool F8 = false, bool MC = false>
 int launch_occ(const AttnArgs& a, int batch, hipStream_t s) {
   const int nblk = (a.nq + 16 * QSUB * NW - 1) / (16 * QSUB * NW) * a.heads * batch;
-  hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, NW, OCC, F8>), dim3(nblk), dim3(64 * NW), 0, s, a);
+  hipLaunchKernelGGL((attn32_kernel<DP, QSUB, ONES, NW, OCC, F8, MC>), dim3(nblk), dim3(64 * NW), 0, s, a);
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
 
-template <int DP, bool F8 = false>
-int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
+int g_attn_maxcol = 1;   // tuning / A-B hook: 0 keeps the per-score FMA (no max column)
+
+template <int DP, bool F8 = false, bool MC = false>
+int launch32_dp_mc(const AttnArgs& a, int batch, hipStream_t s) {
   // query subtiles per wave: as many as stay spill-free (the ONES variant has no l registers)
   constexpr int QS1 = DP <= 48 ? 4 : (DP <= 96 ? 2 : 1);
   constexpr int QS0 = DP <= 96 ? 2 : 1;
@@ -608,10 +666,21 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
     // CU whose phases drift apart, so one block's softmax VALU runs beside the other's MFMAs
     // (N=4096: 295 -> 265 us against one 8-wave block of 4 subtiles); needs >= 2 blocks per CU
     const int nblk2 = (a.nq + 255) / 256 * a.heads * batch;
-    if (a.d == DP - 8 && g_attn_waves == 0 && nblk2 >= 512) return launch_occ<DP, 2, true, 8, 2, F8>(a, batch, s);
+    if (a.d == DP - 8 && g_attn_waves == 0 && nblk2 >= 512)
+      return launch_occ<DP, 2, true, 8, 2, F8, MC>(a, batch, s);
   }
-  if (a.d == DP - 8) return launch32_cfg<DP, QS1, true, F8>(a, batch, s);
-  return launch32_cfg<DP, QS0, false, F8>(a, batch, s);
+  if (a.d == DP - 8) return launch32_cfg<DP, QS1, true, F8, MC>(a, batch, s);
+  return launch32_cfg<DP, QS0, false, F8, MC>(a, batch, s);
+}
+
+template <int DP, bool F8 = false>
+int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
+  // the max column pays at head_dim 40 (N=4096: 273 -> 252 us); at 80 it costs occupancy
+  // (134 vs 122 VGPRs: 39.7 -> 41.0 us), so it is kept to DP = 48
+  if constexpr (DP == 48) {
+    if (g_attn_maxcol && a.d % 8 == 0) return launch32_dp_mc<DP, F8, true>(a, batch, s);
+  }
+  return launch32_dp_mc<DP, F8, false>(a, batch, s);
 }
 
 // fp8 P.V forward (bf16 inputs with 16-byte rows only)
@@ -1033,6 +1102,7 @@ extern "C" int ldm_attention_fp8(const ldm_attn_params* q, ldm_stream_t stream) 
 extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 || waves == 8) ? waves : 0; }
 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
+extern "C" void ldm_attention_set_maxcol(int enabled) { g_attn_maxcol = enabled; }
 
 extern "C" int ldm_attention_fwd_lse(const ldm_attn_params* q, float* lse, ldm_stream_t stream) {
   const int st = attn_validate(q);

@@ -66,6 +66,7 @@ EXPORTS = {
     "ldm_conv2d_set_halo": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp]),
+    "ldm_attention_set_maxcol": (None, [_i]),
     "ldm_group_norm_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
     "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _i, _i, _vp, _i, _vp]),
     "ldm_layer_norm": (_i, [_vp, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp]),
@@ -461,6 +462,11 @@ def set_attention_waves(waves=0):
     """Tuning hook: 4 or 8 waves per flash-attention block (8: every K/V tile serves twice the
     queries); 0 = automatic (8 when that still gives >= 256 blocks)."""
     load_library().ldm_attention_set_waves(int(waves))
+
+
+def set_attention_maxcol(enabled=True):
+    """Tuning hook: scale and running max carried in the Q.K^T head-dim padding (default on)."""
+    load_library().ldm_attention_set_maxcol(int(bool(enabled)))
 
 
 def force_attention_legacy(legacy=True):
