@@ -107,6 +107,10 @@ void ldm_conv2d_set_raster_group(int group_m);
 /* Tuning hook: the halo-tiled 3x3 kernel (bf16, stride 1, 64-channel-aligned sources, output
  * width 64 or 32): 0 = planner's choice, 1 = never, 2 = whenever legal. */
 void ldm_conv2d_set_halo(int mode);
+/* Tuning hook: bf16 NHWC epilogue of the 2-blocks-per-CU tiles — 0 = bias / time embedding /
+ * activation applied from the accumulators and the tile staged once as bf16 (default),
+ * 1 = fp32 staging in row halves (the round-1 form). */
+void ldm_conv2d_set_epilogue(int mode);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).

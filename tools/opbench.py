@@ -165,9 +165,11 @@ def main():
                     help="conv tile plans to compare: 'auto' or 'bm,bn,ksplit[,stages]' (e.g. 256,160,1 or 128,160,8,4)")
     ap.add_argument("--groups", nargs="*", type=int, default=[8], help="conv tile-raster groups to compare")
     ap.add_argument("--lib", default=None, help="load this library build instead (e.g. exp/libabl1.so)")
+    ap.add_argument("--epi", type=int, default=0, help="conv epilogue mode (ldm_conv2d_set_epilogue)")
     a = ap.parse_args()
     if a.lib:
         K.load_library(os.path.abspath(a.lib))
+    K.set_conv_epilogue(a.epi)
     names = a.only or list(CASES)
     built = {}
     for n in names:

@@ -51,6 +51,7 @@ struct ConvArgs {
                       // the stored output (zeroed by the caller; each tile adds one fp32 partial
                       // per gn_unit-channel unit atomically, into slot (tile row index) % gn_slots)
   int gn_unit, gn_slots;
+  int epi_pre;        // 1: the bf16 pre-activated staging epilogue where legal (A/B hook)
   int tap_inner;      // K tiles visited channel-block-major, taps inner (see k_state)
   int group_m;        // M panels per raster group (grouped_tile); 1 = plain row-major tiles
 };
@@ -472,12 +473,16 @@ __device__ __forceinline__ bool fast_temb_ok(const ConvArgs& p, int m0, int rows
   return !p.temb || (min(m0 + rows, p.M) - 1) / p.hw_out - m0 / p.hw_out <= 1;
 }
 
-template <int ROWS, int COLS, int NT>
-__device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0, const float* stage, int pitch,
+// PRE: the staged tile already holds the final pre-residual values as bf16 (bias, time
+// embedding and activation applied from the accumulators by the caller, `pitch` in bf16
+// elements); only the residual, the stores and the GroupNorm statistics are left.
+template <int ROWS, int COLS, int NT, bool PRE = false>
+__device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0, const void* stage_v, int pitch,
                                               float* red) {
   const int tid = threadIdx.x;
   const int N = p.n;
-  if (p.out_layout == LDM_OUT_GEGLU) {
+  const float* stage = reinterpret_cast<const float*>(stage_v);
+  if (!PRE && p.out_layout == LDM_OUT_GEGLU) {
     constexpr int OCW = COLS / 16;             // 8-wide output chunks per row
     constexpr int ORP = NT / OCW;
     constexpr int ONP = (ROWS + ORP - 1) / ORP;
@@ -531,7 +536,8 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
     float add[8];
 #pragma unroll
     for (int k = 0; k < 8; k += 4) {
-      const float4 b4 = p.bias ? *reinterpret_cast<const float4*>(p.bias + n + k) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 b4 = (!PRE && p.bias) ? *reinterpret_cast<const float4*>(p.bias + n + k)
+                                         : make_float4(0.f, 0.f, 0.f, 0.f);
       add[k] = b4.x; add[k + 1] = b4.y; add[k + 2] = b4.z; add[k + 3] = b4.w;
     }
     const bf16_t* res = reinterpret_cast<const bf16_t*>(p.residual);
@@ -540,7 +546,7 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
     const int b0 = m0 / p.hw_out;
     const int bsplit = (b0 + 1) * p.hw_out;          // first row of batch b0 + 1
     float4 te0[2], te1[2];
-    if (p.temb) {
+    if (!PRE && p.temb) {
       const float* tp = p.temb + (int64_t)b0 * p.temb_stride + n;
       te0[0] = *reinterpret_cast<const float4*>(tp);
       te0[1] = *reinterpret_cast<const float4*>(tp + 4);
@@ -567,21 +573,26 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
         const int r = r0 + (q0 + q) * RP;
         const int m = m0 + r;
         if (q0 + q >= NP || r >= ROWS || m >= p.M) break;
-        const float* srow = stage + r * pitch + 8 * c8;
-        const float4 x0 = *reinterpret_cast<const float4*>(srow);
-        const float4 x1 = *reinterpret_cast<const float4*>(srow + 4);
-        float v[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        float v[8];
+        if constexpr (PRE) {
+          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(stage_v) + r * pitch + 8 * c8), v);
+        } else {
+          const float* srow = stage + r * pitch + 8 * c8;
+          const float4 x0 = *reinterpret_cast<const float4*>(srow);
+          const float4 x1 = *reinterpret_cast<const float4*>(srow + 4);
+          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] += add[k];
-        if (p.temb) {
-          const bool second = m >= bsplit;
-          const float4 ta = second ? te1[0] : te0[0], tb = second ? te1[1] : te0[1];
-          v[0] += ta.x; v[1] += ta.y; v[2] += ta.z; v[3] += ta.w;
-          v[4] += tb.x; v[5] += tb.y; v[6] += tb.z; v[7] += tb.w;
-        }
-        if (p.act != LDM_ACT_NONE) {
+          for (int k = 0; k < 8; ++k) v[k] += add[k];
+          if (p.temb) {
+            const bool second = m >= bsplit;
+            const float4 ta = second ? te1[0] : te0[0], tb = second ? te1[1] : te0[1];
+            v[0] += ta.x; v[1] += ta.y; v[2] += ta.z; v[3] += ta.w;
+            v[4] += tb.x; v[5] += tb.y; v[6] += tb.z; v[7] += tb.w;
+          }
+          if (p.act != LDM_ACT_NONE) {
 #pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = act_f(v[k], p.act);
+            for (int k = 0; k < 8; ++k) v[k] = act_f(v[k], p.act);
+          }
         }
         if (res) {
           float rr[8];
@@ -590,7 +601,11 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
           for (int k = 0; k < 8; ++k) v[k] += rr[k];
         }
         const uint4 packed = pack8(v);
+#ifdef LDM_ABL_EPI_NO_STORE   // ablation build: the epilogue's math kept, its global stores dropped
+        if (packed.x == 0x12345678u && packed.y == 0x9abcdef0u) *reinterpret_cast<uint4*>(out + (int64_t)m * N + n) = packed;
+#else
         *reinterpret_cast<uint4*>(out + (int64_t)m * N + n) = packed;
+#endif
         if (stats) {
           float st[8];
           unpack8(packed, st);                   // statistics of the value as stored
@@ -958,6 +973,47 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     return;
   }
 #endif
+  // ------------------------------------------------------------------ bf16 NHWC epilogue
+  // Bias, time embedding and activation are applied straight from the accumulators (a lane holds
+  // 4 consecutive channels of one row), the tile is staged ONCE as bf16 [BM][BN + 8] (half the
+  // LDS bytes of the fp32 staging, one barrier instead of three: the two blocks of a CU share the
+  // LDS with each other's main loop, whose operand reads it is bound by), and rows leave as 16-B
+  // stores with the residual and GroupNorm statistics.  (Rounding: act(acc + bias) is rounded to
+  // bf16 before the residual add.)
+  if constexpr (sizeof(T) == 2 && BM >= 64) {
+    constexpr int HP = BN + 8;
+    static_assert(BM * HP * 2 <= SMEM * 16, "bf16 stage exceeds LDS");
+    if (p.epi_pre && p.ksplit == 1 && p.out_layout == LDM_OUT_NHWC && fast_epilogue_ok(p) &&
+        fast_temb_ok(p, m0, BM)) {
+      bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int nl = wn * (BN / 2) + j * 16 + 4 * g;
+        const int n = n0 + nl;
+        float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (p.bias && n < p.n) b4 = *reinterpret_cast<const float4*>(p.bias + n);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int ml = wm * (BM / 2) + i * 16 + lr;
+          const int m = m0 + ml;
+          float v[4] = {acc[i][j][0] + b4.x, acc[i][j][1] + b4.y, acc[i][j][2] + b4.z, acc[i][j][3] + b4.w};
+          if (p.temb && n < p.n && m < p.M) {
+            const float4 t4 = *reinterpret_cast<const float4*>(p.temb + (int64_t)(m / p.hw_out) * p.temb_stride + n);
+            v[0] += t4.x; v[1] += t4.y; v[2] += t4.z; v[3] += t4.w;
+          }
+          if (p.act != LDM_ACT_NONE) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = act_f(v[r], p.act);
+          }
+          bf16_t h[4] = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+          *reinterpret_cast<uint2*>(hs + ml * HP + nl) = *reinterpret_cast<const uint2*>(h);
+        }
+      }
+      __syncthreads();
+      epilogue_fast<BM, BN, 256, true>(p, m0, n0, hs, HP, reinterpret_cast<float*>(smem));
+      return;
+    }
+  }
   // ------------------------------------------------------------------ fused epilogue
   // phase 1: raw accumulators -> LDS [EPI_ROWS][PITCH] fp32 (per row half when EPI_H == 2:
   // wave row wm owns rows [wm * BM/2, (wm+1) * BM/2) = half wm)
@@ -972,7 +1028,11 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
 #pragma unroll
   for (int h = 0; h < EPI_H; ++h) {
     if (h > 0) __syncthreads();   // the previous half (and its reduction scratch) is consumed
+#ifdef LDM_ABL_EPI_NO_STAGE   // ablation build: phase 1 (accumulators -> LDS) dropped
+    if (acc[0][0][0] == 12345.f) {
+#else
     if (EPI_H == 1 || wm == h) {
+#endif
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int ml = (EPI_H == 1 ? wm * (BM / 2) : 0) + i * 16 + lr;
@@ -985,6 +1045,9 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
       }
     }
     __syncthreads();
+#ifdef LDM_ABL_EPI_STAGE_ONLY  // ablation build: phase 2 (rows out of LDS, math, stores) dropped
+    if (stage[tid] != 12345.f) continue;
+#endif
     // phase 2: coalesced rows
     const int mh = m0 + h * EPI_ROWS;
     if (p.ksplit > 1) {
@@ -1490,6 +1553,7 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
 // halo plan: bf16 3x3 stride-1 conv, no upsample, 64-channel-aligned sources, an output width
 // the kernel is instantiated for, whole output rows per tile
 int g_halo_mode = 0;   // tuning hook: 0 planner, 1 never, 2 whenever legal
+int g_epi_pre = 1;     // tuning hook: bf16 pre-activated staging epilogue (1) or fp32 staging (0)
 bool halo_legal(const ldm_conv_params* q, int es) {
   if (es != 2 || q->ksize != 3 || q->stride != 1 || q->upsample || q->pad_mode != 0) return false;
   if (q->c0 % 64 || q->c1 % 64 || q->kpad != 9 * (q->c0 + q->c1)) return false;
@@ -1756,6 +1820,7 @@ extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
 int g_group_m = 8;
 extern "C" void ldm_conv2d_set_raster_group(int g) { g_group_m = g >= 1 ? g : 8; }
 extern "C" void ldm_conv2d_set_halo(int mode) { g_halo_mode = (mode == 1 || mode == 2) ? mode : 0; }
+extern "C" void ldm_conv2d_set_epilogue(int mode) { g_epi_pre = mode == 1 ? 0 : 1; }
 extern "C" void ldm_conv2d_force_stages(int stages) {
   g_force_stages = (stages == 1 || stages == 3 || stages == 4) ? stages : 0;   // 1: register-staged operands
 }
@@ -1812,6 +1877,7 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.gn_part = reinterpret_cast<double*>(q->gn_partial);
   a.gn_unit = q->gn_unit > 0 ? q->gn_unit : 1;
   a.gn_slots = q->gn_slots > 0 ? q->gn_slots : 1;
+  a.epi_pre = g_epi_pre;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (use_halo) return launch_halo(a, s);
   if (pl.bm == 256) return launch_big(a, s);

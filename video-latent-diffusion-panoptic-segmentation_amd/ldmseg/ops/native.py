@@ -64,6 +64,7 @@ EXPORTS = {
     "ldm_conv2d_force_stages": (None, [_i]),
     "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_conv2d_set_halo": (None, [_i]),
+    "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_set_maxcol": (None, [_i]),
@@ -487,6 +488,11 @@ def set_conv_raster_group(group_m=8):
 def set_conv_halo(mode=0):
     """Tuning hook: halo-tiled 3x3 kernel — 0 planner, 1 never, 2 whenever legal."""
     load_library().ldm_conv2d_set_halo(int(mode))
+
+
+def set_conv_epilogue(mode=0):
+    """Tuning hook: 0 bf16 pre-activated staging epilogue (default), 1 fp32 staging."""
+    load_library().ldm_conv2d_set_epilogue(int(mode))
 
 
 def force_conv_plan(bm=0, bn=0, ksplit=1):
