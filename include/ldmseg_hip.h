@@ -136,9 +136,10 @@ int ldm_attention_fp8(const ldm_attn_params* p, ldm_stream_t stream);
 /* Tuning hook (benchmarks / tests only): 1 routes bf16 through the 16x16x16-MFMA kernel
  * instead of the 16x16x32 one; 0 restores the default. */
 void ldm_attention_force_legacy(int legacy);
-/* Tuning hook (A/B only): 1 (default) carries the softmax scale and running max in the Q.K^T
- * head-dim padding when head_dim % 32 != 0 (no per-score FMA); 0 restores the FMA form. */
-void ldm_attention_set_maxcol(int enabled);
+/* Tuning hook (A/B only), head_dim 40: 2 (default) the 32x32x16-MFMA kernel; 1 the 16x16x32 kernel
+ * with the softmax scale and running max carried in the Q.K^T head-dim padding; 0 the 16x16x32
+ * kernel with one FMA per score. */
+void ldm_attention_set_maxcol(int mode);
 /* Tuning hook: waves per block of the bf16 flash-attention kernel (4 or 8; 0 = automatic). */
 void ldm_attention_set_waves(int waves);
 /* Training forward: as ldm_attention, and also stores lse[(b * heads + h) * n_q + q] =

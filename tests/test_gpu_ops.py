@@ -216,13 +216,13 @@ def test_attention_softmax_spike():
     assert rel_err(o, ref) < 1e-4
 
 
-@pytest.mark.parametrize("maxcol", [True, False])
-@pytest.mark.parametrize("C,N", [(320, 520), (640, 300), (320, 4096)])
+@pytest.mark.parametrize("maxcol", [2, 1, 0])
+@pytest.mark.parametrize("C,N", [(320, 520), (640, 300), (320, 4096), (320, 77)])
 def test_attention_softmax_spike_bf16(C, N, maxcol):
     """bf16 kernel under forced rescales, with and without the max column (scale and running max
     carried in the Q.K^T head-dim padding): a huge logit in the last kv tile, a first kv tile
     whose logits are all very negative for some rows (the first-tile max must still be taken),
-    and a row whose max grows tile after tile."""
+    and a row whose max grows tile after tile.  maxcol 2: the 32x32x16 head_dim-40 kernel."""
     torch.manual_seed(14)
     B = 1
     q, k, v = torch.randn(B, N, C), torch.randn(B, N, C), torch.randn(B, N, C)
@@ -236,7 +236,7 @@ def test_attention_softmax_spike_bf16(C, N, maxcol):
     try:
         o = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, 8, C // 8, N, N, 3 * C, 3 * C, 3 * C)
     finally:
-        K.set_attention_maxcol(True)
+        K.set_attention_maxcol(2)
     assert rel_err(o, ref) < 2e-2
     assert (o.float() - ref.to(DEV)).abs().max().item() < 0.05
 

@@ -47,7 +47,7 @@ def mm_case(M, K, N):
     return (lambda: torch.mm(a, b)), 2.0 * M * K * N, None
 
 
-def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=True):
+def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
     def run():
@@ -137,8 +137,9 @@ CASES = {
     "mm_conv_l2_1280": lambda: mm_case(2048, 11520, 1280),
     "mm_conv_l3_1280": lambda: mm_case(512, 11520, 1280),
     "attn_4096_d40": lambda: attn_case(8, 4096, 320),
-    "attn_4096_d40_fma": lambda: attn_case(8, 4096, 320, maxcol=False),
-    "attn_1024_d80_fma": lambda: attn_case(8, 1024, 640, maxcol=False),
+    "attn_4096_d40_fma": lambda: attn_case(8, 4096, 320, maxcol=0),
+    "attn_4096_d40_mc16": lambda: attn_case(8, 4096, 320, maxcol=1),
+    "attn_1024_d80_fma": lambda: attn_case(8, 1024, 640, maxcol=0),
     "attn_4096_d40_legacy": lambda: attn_case(8, 4096, 320, legacy=True),
     "attn_1024_d80_legacy": lambda: attn_case(8, 1024, 640, legacy=True),
     "attn_256_d160_legacy": lambda: attn_case(8, 256, 1280, legacy=True),

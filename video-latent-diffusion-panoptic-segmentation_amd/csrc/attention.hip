@@ -629,6 +629,208 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
   }
 }
 
+// ======================================================================================
+// head_dim 40 (the UNet's 64x64 level: 4096 tokens, ~90 % of the attention time) on the
+// 32x32x16 MFMA.  Per wave: 32 queries; per 64-key tile:
+//   S^T[kv][q] = K Q^T   two 32-key blocks x three 16-wide head-dim chunks = 6 MFMAs (x16
+//                        padding of d = 40 -> 48 instead of the x32 padding -> 64 of the
+//                        16x16x32 form: 6 issues instead of 16);
+//   O^T[d][q] += V^T P^T two 32-row head-dim blocks x four 16-key steps = 8 MFMAs; the B operand
+//                        is the S^T accumulator converted in place (a 32x32 result has its column
+//                        on the lane and its rows in registers; k order 16s + 8(j>>2) + 4h + (j&3)),
+//                        the A operand two ds_read_b64_tr_b16 of the row-major V tile in that order.
+// The row max is a tree over the lane's 32 scores plus one permlane32 swap.  Scale and running
+// max ride in the head-dim padding (Q prescaled, Q[:, 40] = -m, K[:, 40] = 1), the softmax
+// denominator in V's ones column (d = 40), as in attn32_kernel's MC / ONES forms.
+template <int NW, int OCC, int KT = 64>
+__global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p) {
+  typedef bf16_t T;
+  typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+  constexpr int EPC = 8, CPR = 8, RCH = CPR + 1, ROW = RCH * EPC, TILE = KT * ROW, ES = 2;
+  __shared__ uint4 smem[2 * 2 * TILE * ES / 16];
+  T* const lds = reinterpret_cast<T*>(smem);
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5, i16 = lane & 15;
+  int qb, h, b;
+  {
+    const int nqb = (p.nq + 32 * NW - 1) / (32 * NW);
+    const int bid = blockIdx.x, nblk = gridDim.x;
+    const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
+    const int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    qb = t % nqb;
+    const int hb = t / nqb;
+    h = hb % p.heads;
+    b = hb / p.heads;
+  }
+  const int qbase = qb * (32 * NW) + wave * 32;
+  const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
+  const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
+  const T* vp = reinterpret_cast<const T*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * p.d;
+  constexpr int ONES_CHUNK = 5;                     // d = 40: V ones column, K max column
+
+  auto issue_tile = [&](int kv0, int buf) {
+    const unsigned kb = lds0 + (unsigned)(buf * 2 * TILE * ES);
+    const unsigned vb = kb + TILE * ES;
+    for (int i = wave; i < RCH * (KT / 64); i += NW) {
+      const int L = i * 64 + lane;
+      const int row = L / RCH, c = L - row * RCH;
+      const int kv = kv0 + row, d = c * EPC;
+      const bool ok = kv < p.nkv && c < CPR && d < p.d;
+      const bool kone = c == ONES_CHUNK && kv < p.nkv;
+      const void* ks = ok ? (const void*)(kp + (int64_t)kv * p.ks + d)
+                          : (kone ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
+      const void* vs = ok ? (const void*)(vp + (int64_t)kv * p.vs + d)
+                          : (c == ONES_CHUNK ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
+      const unsigned off = __builtin_amdgcn_readfirstlane(i * 64 * 16);
+      glds16(ks, kb + off);
+      glds16(vs, vb + off);
+    }
+  };
+  const float c2 = p.scale_log2;
+
+  // Q^T (B operand) chunk c: lane holds Q[q = qbase + r32][d = 16c + 8hh .. +8] * c2; the max
+  // column d = 40 is element 0 of chunk 2 in the hh = 1 lanes (initially -m = 0)
+  uint4 qf[3];
+  {
+    const int qi = qbase + r32;
+    const T* qrow = qp + (int64_t)qi * p.qs;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const int dd = 16 * c + 8 * hh;
+      if (qi < p.nq && dd < p.d) qf[c] = scale_bf16x8(*reinterpret_cast<const uint4*>(qrow + dd), c2);
+      else qf[c] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  f32x16_t oacc[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[db][r] = 0.f;
+  float mq = 0.f;
+
+  typedef __attribute__((ext_vector_type(4))) short s4_t;
+  typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+  auto compute = [&](int buf, int kv0, bool masked, bool first, int half) {
+    const T* Ks = lds + buf * 2 * TILE + half * 64 * ROW;
+    const T* Vs = lds + buf * 2 * TILE + TILE + half * 64 * ROW;
+    kv0 += 64 * half;
+    first = first && half == 0;
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[blk][r] = 0.f;
+      const T* krow = Ks + (32 * blk + r32) * ROW + 8 * hh;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const uint4 ka = *reinterpret_cast<const uint4*>(krow + 16 * c);
+        sacc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, ka),
+                                                            __builtin_bit_cast(bf16x8_t, qf[c]), sacc[blk], 0, 0, 0);
+      }
+    }
+    if (masked) {
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (kv0 + 32 * blk + 8 * (r >> 2) + 4 * hh + (r & 3) >= p.nkv) sacc[blk][r] = -INFINITY;
+    }
+    float mx;
+    {
+      float t[11];
+#pragma unroll
+      for (int k = 0; k < 10; ++k) {
+        const int a = 3 * k;
+        t[k] = vmax3(a < 16 ? sacc[0][a] : sacc[1][a - 16], a + 1 < 16 ? sacc[0][a + 1] : sacc[1][a + 1 - 16],
+                     a + 2 < 16 ? sacc[0][a + 2] : sacc[1][a + 2 - 16]);
+      }
+      t[10] = __builtin_elementwise_maximum(sacc[1][14], sacc[1][15]);
+      const float u0 = vmax3(t[0], t[1], t[2]), u1 = vmax3(t[3], t[4], t[5]), u2 = vmax3(t[6], t[7], t[8]);
+      mx = vmax3(vmax3(u0, u1, u2), t[9], t[10]);
+      unsigned w = __float_as_uint(mx);
+      const auto sw = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+      mx = vmax3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), mx);
+    }
+    // accumulators are s * c2 - m already; the first tile always sets m (from m = 0)
+    if (first || __any(mx > kRescaleThr)) {
+      const float tgt = mq + mx;
+      const float mn = bf16_rne(first ? tgt : fmaxf(mq, tgt));
+      const float delta = mn - mq;
+      const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);   // (O = 0 on the first tile)
+      mq = mn;
+      oacc[0] *= alpha;
+      oacc[1] *= alpha;
+      sacc[0] -= delta;
+      sacc[1] -= delta;
+      if (hh == 1) qf[2].x = (qf[2].x & 0xffff0000u) | (__float_as_uint(-mn) >> 16);
+    }
+    uint4 pb[2][2];                           // bf16 P^T fragment of k-step (block, s)
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        float pv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pv[j] = __builtin_amdgcn_exp2f(sacc[blk][8 * st + j]);
+        pb[blk][st] = make_uint4(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]), pack_bf16x2(pv[4], pv[5]),
+                                 pack_bf16x2(pv[6], pv[7]));
+      }
+    // O^T += V^T P^T: A = V^T rows d (block db) for keys 16s' + {4hh..+3, 8 + 4hh..+3} of block blk
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int cb = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const T* a0 = Vs + (32 * blk + 16 * st + 4 * hh + (i16 >> 2)) * ROW + cb;
+          const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0)));
+          const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0 + 8 * ROW)));
+          const uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, va),
+                                                             __builtin_bit_cast(bf16x8_t, pb[blk][st]), oacc[db], 0, 0, 0);
+        }
+    }
+  };
+
+  const int ntiles = (p.nkv + KT - 1) / KT;
+  const int nfull = p.nkv / KT;
+  issue_tile(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nfull; ++t) {
+    if (t + 1 < ntiles) issue_tile((t + 1) * KT, (t + 1) & 1);
+#pragma unroll
+    for (int hf = 0; hf < KT / 64; ++hf) compute(t & 1, t * KT, false, t == 0, hf);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (nfull < ntiles) {
+    for (int hf = 0; hf < KT / 64 && nfull * KT + 64 * hf < p.nkv; ++hf) compute(nfull & 1, nfull * KT, true, nfull == 0, hf);
+  }
+
+  // denominator: O^T row d = 40 = block 1 register 4 of the hh = 0 lane of this column
+  const float lt = __shfl(oacc[1][4], r32, 64);
+  const float inv = 1.0f / lt;
+  const int qi = qbase + r32;
+  if (qi < p.nq) {
+    if (p.lse && hh == 0) p.lse[((int64_t)b * p.heads + h) * p.nq + qi] = mq + __log2f(lt);
+    T* orow = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * p.d + (int64_t)qi * p.os;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = 8 * g4 + 4 * hh;
+      *reinterpret_cast<uint2*>(orow + d) =
+          make_uint2(pack_bf16x2(oacc[0][4 * g4] * inv, oacc[0][4 * g4 + 1] * inv),
+                     pack_bf16x2(oacc[0][4 * g4 + 2] * inv, oacc[0][4 * g4 + 3] * inv));
+    }
+    *reinterpret_cast<uint2*>(orow + 32 + 4 * hh) =
+        make_uint2(pack_bf16x2(oacc[1][0] * inv, oacc[1][1] * inv), pack_bf16x2(oacc[1][2] * inv, oacc[1][3] * inv));
+  }
+}
+
 int g_attn_waves = 0;   // 0: auto (8 when that still gives >= 256 blocks), 4 or 8: forced
 
 template <int DP, int QSUB, bool ONES, bool F8 = false, bool MC = false>
@@ -655,6 +857,7 @@ int launch_occ(const AttnArgs& a, int batch, hipStream_t s) {
 }
 
 int g_attn_maxcol = 1;   // tuning / A-B hook: 0 keeps the per-score FMA (no max column)
+int g_attn_d40 = 1;      // tuning / A-B hook: 0 routes head_dim 40 to the 16x16x32 kernel
 
 template <int DP, bool F8 = false, bool MC = false>
 int launch32_dp_mc(const AttnArgs& a, int batch, hipStream_t s) {
@@ -678,6 +881,22 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
   // the max column pays at head_dim 40 (N=4096: 273 -> 252 us); at 80 it costs occupancy
   // (134 vs 122 VGPRs: 39.7 -> 41.0 us), so it is kept to DP = 48
   if constexpr (DP == 48) {
+    if (!F8 && g_attn_d40 && a.d == 40) {
+      // 32x32x16 kernel: 8 waves x 32 queries, two blocks per CU when there are >= 512 blocks
+      const int nblk = (a.nq + 255) / 256 * a.heads * batch;
+      // (measured at N=4096: 8 waves x 2 blocks per CU 241 us; 4 waves x 4 blocks 302 us — each K/V
+      // tile then serves half the queries; 128-key tiles 249 us)
+      if (g_attn_waves == 4) {
+        const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
+        hipLaunchKernelGGL((attn_d40_kernel<4, 4>), dim3(nb4), dim3(256), 0, s, a);
+      } else if (nblk >= 512 || g_attn_waves == 8) hipLaunchKernelGGL((attn_d40_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a);
+      else {
+        const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
+        hipLaunchKernelGGL((attn_d40_kernel<4, 2>), dim3(nb4), dim3(256), 0, s, a);
+      }
+      LDM_CHECK_LAUNCH();
+      return LDM_OK;
+    }
     if (g_attn_maxcol && a.d % 8 == 0) return launch32_dp_mc<DP, F8, true>(a, batch, s);
   }
   return launch32_dp_mc<DP, F8, false>(a, batch, s);
@@ -1102,7 +1321,10 @@ extern "C" int ldm_attention_fp8(const ldm_attn_params* q, ldm_stream_t stream) 
 extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 || waves == 8) ? waves : 0; }
 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
-extern "C" void ldm_attention_set_maxcol(int enabled) { g_attn_maxcol = enabled; }
+extern "C" void ldm_attention_set_maxcol(int mode) {
+  g_attn_maxcol = mode >= 1 ? 1 : 0;     // 0: per-score FMA, 16x16x32 kernel
+  g_attn_d40 = mode >= 2 ? 1 : 0;        // 1: max column, 16x16x32 kernel; 2: 32x32x16 d = 40 kernel
+}
 
 extern "C" int ldm_attention_fwd_lse(const ldm_attn_params* q, float* lse, ldm_stream_t stream) {
   const int st = attn_validate(q);

@@ -465,9 +465,10 @@ def set_attention_waves(waves=0):
     load_library().ldm_attention_set_waves(int(waves))
 
 
-def set_attention_maxcol(enabled=True):
-    """Tuning hook: scale and running max carried in the Q.K^T head-dim padding (default on)."""
-    load_library().ldm_attention_set_maxcol(int(bool(enabled)))
+def set_attention_maxcol(mode=2):
+    """Tuning hook (head_dim 40): 2 the 32x32x16 kernel (default), 1 the 16x16x32 kernel with the
+    scale and running max in the Q.K^T padding, 0 the 16x16x32 kernel with an FMA per score."""
+    load_library().ldm_attention_set_maxcol(int(mode))
 
 
 def force_attention_legacy(legacy=True):
