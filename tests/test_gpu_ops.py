@@ -147,6 +147,42 @@ def test_linear_and_geglu(M, Kd, N, dt):
     assert rel_err(g, h * F.gelu(gate)) < tol(dt)
 
 
+@pytest.mark.parametrize("M,C", [(4096, 320), (1024, 640), (256, 1280), (333, 320)])
+def test_linear_layernorm_fold(M, C):
+    """norm -> Linear as ONE GEMM on the raw rows: the producer GEMM (with a residual) sums each
+    stored row's (sum, sumsq) in its epilogue (row_stats), the consumer applies
+    rstd (x W'^T - mean c1) + W beta + b in its epilogue (packed_ln_fold) — NHWC (QKV) and GEGLU
+    (ff.net.0) outputs, against torch fp32 LayerNorm + Linear on the same bf16 rows."""
+    torch.manual_seed(21)
+    x = (torch.randn(M, C) * 1.5 + 0.7).to(DEV, torch.bfloat16)
+    res = torch.randn(M, C).to(DEV, torch.bfloat16)
+    prod = torch.nn.Linear(C, C)
+    pp = K.PackedConv(prod.weight.to(DEV), prod.bias.to(DEV), torch.bfloat16)
+    rows = torch.zeros(M, 2, device=DEV)
+    h = K.linear(pp, x, residual=res, row_stats=rows)
+    hf = h.float()
+    assert torch.allclose(rows[:, 0], hf.sum(1), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(rows[:, 1], (hf * hf).sum(1), rtol=1e-4, atol=1e-1)
+    ln = torch.nn.LayerNorm(C)
+    with torch.no_grad():
+        ln.weight.uniform_(0.5, 1.5)
+        ln.bias.normal_(0, 0.2)
+    qkv = torch.nn.Linear(C, 3 * C, bias=False)
+    pq = K.packed_ln_fold(qkv.weight.to(DEV), None, ln.weight.to(DEV), ln.bias.to(DEV), torch.bfloat16)
+    out = K.linear(pq, h, ln=(rows, 1e-5))
+    with torch.no_grad():
+        n = ln.to(DEV)(hf)
+        ref = n @ qkv.weight.to(DEV).t()
+    assert rel_err(out, ref) < 2e-2
+    ff = torch.nn.Linear(C, 8 * C)
+    pf = K.packed_ln_fold(ff.weight.to(DEV), ff.bias.to(DEV), ln.weight.to(DEV), ln.bias.to(DEV), torch.bfloat16,
+                          geglu=True)
+    g = K.linear(pf, h, out_layout=K.OUT_GEGLU, ln=(rows, 1e-5))
+    with torch.no_grad():
+        a, gate = (n @ ff.weight.to(DEV).t() + ff.bias.to(DEV)).chunk(2, dim=-1)
+    assert rel_err(g, a * F.gelu(gate)) < 2e-2
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 def test_conv_transpose_shuffle(dt):
     torch.manual_seed(2)

@@ -150,6 +150,10 @@ CASES = {
     "attn_256_d160": lambda: attn_case(8, 256, 1280),
     "gn_l0_fused": lambda: gn_case(8, 4096, 320, True),
     "gn_l0_unfused": lambda: gn_case(8, 4096, 320, False),
+    "gn_l1_fused": lambda: gn_case(8, 1024, 640, True),
+    "gn_l2_fused": lambda: gn_case(8, 256, 1280, True),
+    "gn_l3_fused": lambda: gn_case(8, 64, 1280, True),
+    "gn_up0_fused": lambda: gn_case(8, 4096, 960, True),
     "ln_l0": lambda: ln_case(32768, 320),
     "panoptic_k128_512": lambda: panoptic_case(8, 128, 512, 512),
     "panoptic_k30_512": lambda: panoptic_case(8, 30, 512, 512),

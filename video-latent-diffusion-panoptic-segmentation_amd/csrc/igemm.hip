@@ -52,6 +52,10 @@ struct ConvArgs {
                       // per gn_unit-channel unit atomically, into slot (tile row index) % gn_slots)
   int gn_unit, gn_slots;
   int epi_pre;        // 1: the bf16 pre-activated staging epilogue where legal (A/B hook)
+  float* row_stats;   // optional [M][2] (sum, sumsq) of every stored output row (atomic adds)
+  const float* ln_rows;   // optional LayerNorm fold: [M][2] (sum, sumsq) of the A rows ...
+  const float* ln_c1;     // ... and [n] column sums of the gamma-scaled weight
+  float ln_inv_k, ln_eps;
   int tap_inner;      // K tiles visited channel-block-major, taps inner (see k_state)
   int group_m;        // M panels per raster group (grouped_tile); 1 = plain row-major tiles
 };
@@ -468,6 +472,15 @@ __device__ __forceinline__ uint4 pack8(const float* v) {
   return *reinterpret_cast<const uint4*>(h);
 }
 
+// LayerNorm fold: (rstd, -rstd * mean) of A row m from its (sum, sumsq)
+__device__ __forceinline__ float2 ln_row(const ConvArgs& p, int m) {
+  const float2 st = *reinterpret_cast<const float2*>(p.ln_rows + 2 * (int64_t)m);
+  const float mean = st.x * p.ln_inv_k;
+  const float var = fmaxf(st.y * p.ln_inv_k - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + p.ln_eps);
+  return make_float2(rstd, -rstd * mean);
+}
+
 // rows [m0, m0 + rows) cover at most two batches (the fast path holds two time embeddings)
 __device__ __forceinline__ bool fast_temb_ok(const ConvArgs& p, int m0, int rows) {
   return !p.temb || (min(m0 + rows, p.M) - 1) / p.hw_out - m0 / p.hw_out <= 1;
@@ -532,6 +545,9 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
   for (int hh = 0; hh < HALVES; ++hh)
 #pragma unroll
     for (int k = 0; k < 8; ++k) { s[hh][k] = 0.f; sq[hh][k] = 0.f; }
+  float rsum[NP], rsq[NP];                       // PRE + row_stats: this thread's part of each row
+#pragma unroll
+  for (int q = 0; q < NP; ++q) { rsum[q] = 0.f; rsq[q] = 0.f; }
   if (act) {
     float add[8];
 #pragma unroll
@@ -613,7 +629,39 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
 #pragma unroll
           for (int k = 0; k < 8; ++k) { s[hh][k] += st[k]; sq[hh][k] += st[k] * st[k]; }
         }
+        if (PRE && p.row_stats) {
+          float st[8];
+          unpack8(packed, st);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) { rsum[q0 + q] += st[k]; rsq[q0 + q] += st[k] * st[k]; }
+        }
       }
+    }
+  }
+  if (PRE && p.row_stats) {
+    // reduce each row's CW partials through LDS (rows x CW (sum, sumsq), after every stage read),
+    // then one atomic pair per (row, tile)
+    __syncthreads();
+    if (r0 < RP) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) {
+        const int r = r0 + q * RP;
+        if (r < ROWS) {
+          red[(r * CW + c8) * 2] = rsum[q];
+          red[(r * CW + c8) * 2 + 1] = rsq[q];
+        }
+      }
+    }
+    __syncthreads();
+    for (int r = tid; r < ROWS; r += NT) {
+      if (m0 + r >= p.M) break;
+      float a = 0.f, b = 0.f;
+      for (int c = 0; c < CW && n0 + 8 * c < N; ++c) {
+        a += red[(r * CW + c) * 2];
+        b += red[(r * CW + c) * 2 + 1];
+      }
+      atomicAdd(p.row_stats + 2 * (int64_t)(m0 + r), a);
+      atomicAdd(p.row_stats + 2 * (int64_t)(m0 + r) + 1, b);
     }
   }
   if (!stats) return;
@@ -938,24 +986,40 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     if (p.out_layout == LDM_OUT_GEGLU && p.ksplit == 1 && !p.out_f32 &&
         (reinterpret_cast<uintptr_t>(p.out) & 7) == 0) {
       const int NO = p.n >> 1;
+      float2 lnr[FM];                           // LayerNorm fold: this lane's rows, computed once
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * (BM / 2) + i * 16 + lr;
+        lnr[i] = (p.ln_rows && m < p.M) ? ln_row(p, m) : make_float2(1.f, 0.f);
+      }
 #pragma unroll
       for (int j = 0; j < FN; j += 2) {
         const int pc = n0 + wn * (BN / 2) + j * 16 + 4 * g;   // packed column of the hidden values
         if (pc >= p.n) continue;
         const int oc = (pc >> 5) * 16 + (pc & 15);            // output channel
-        float bh[4], bg[4];
+        float bh[4], bg[4], ch[4], cg[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           bh[r] = p.bias ? p.bias[pc + r] : 0.f;
           bg[r] = p.bias ? p.bias[pc + 16 + r] : 0.f;
+          ch[r] = p.ln_rows ? p.ln_c1[pc + r] : 0.f;
+          cg[r] = p.ln_rows ? p.ln_c1[pc + 16 + r] : 0.f;
         }
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const int m = m0 + wm * (BM / 2) + i * 16 + lr;
           if (m >= p.M) continue;
           float v[4];
+          if (p.ln_rows) {                  // LayerNorm folded: rstd (acc - mean c1) + bias
+            const float2 rs = lnr[i];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = (acc[i][j][r] + bh[r]) * gelu_f(acc[i][j + 1][r] + bg[r]);
+            for (int r = 0; r < 4; ++r)
+              v[r] = fmaf(rs.y, ch[r], fmaf(rs.x, acc[i][j][r], bh[r])) *
+                     gelu_f(fmaf(rs.y, cg[r], fmaf(rs.x, acc[i][j + 1][r], bg[r])));
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = (acc[i][j][r] + bh[r]) * gelu_f(acc[i][j + 1][r] + bg[r]);
+          }
           store4<T>(p.out, (int64_t)m * NO + oc, v, false);
         }
       }
@@ -986,17 +1050,31 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     if (p.epi_pre && p.ksplit == 1 && p.out_layout == LDM_OUT_NHWC && fast_epilogue_ok(p) &&
         fast_temb_ok(p, m0, BM)) {
       bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
+      float2 lnr[FM];                           // LayerNorm fold: this lane's rows, computed once
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wm * (BM / 2) + i * 16 + lr;
+        lnr[i] = (p.ln_rows && m < p.M) ? ln_row(p, m) : make_float2(1.f, 0.f);
+      }
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         const int nl = wn * (BN / 2) + j * 16 + 4 * g;
         const int n = n0 + nl;
-        float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        float4 b4 = make_float4(0.f, 0.f, 0.f, 0.f), c4 = b4;
         if (p.bias && n < p.n) b4 = *reinterpret_cast<const float4*>(p.bias + n);
+        if (p.ln_rows && n < p.n) c4 = *reinterpret_cast<const float4*>(p.ln_c1 + n);
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const int ml = wm * (BM / 2) + i * 16 + lr;
           const int m = m0 + ml;
           float v[4] = {acc[i][j][0] + b4.x, acc[i][j][1] + b4.y, acc[i][j][2] + b4.z, acc[i][j][3] + b4.w};
+          if (p.ln_rows && m < p.M) {       // rstd (acc - mean c1) + bias
+            const float2 rs = lnr[i];
+            v[0] = fmaf(rs.y, c4.x, fmaf(rs.x, acc[i][j][0], b4.x));
+            v[1] = fmaf(rs.y, c4.y, fmaf(rs.x, acc[i][j][1], b4.y));
+            v[2] = fmaf(rs.y, c4.z, fmaf(rs.x, acc[i][j][2], b4.z));
+            v[3] = fmaf(rs.y, c4.w, fmaf(rs.x, acc[i][j][3], b4.w));
+          }
           if (p.temb && n < p.n && m < p.M) {
             const float4 t4 = *reinterpret_cast<const float4*>(p.temb + (int64_t)(m / p.hw_out) * p.temb_stride + n);
             v[0] += t4.x; v[1] += t4.y; v[2] += t4.z; v[3] += t4.w;
@@ -1646,7 +1724,22 @@ int g_force_bm = 0, g_force_bn = 0, g_force_ks = 0;
 
 int clamp_ksplit(int ks, int nk) { return std::max(1, std::min(std::min(ks, nk), 16)); }
 
+Plan make_plan_base(const ldm_conv_params* q, int M, int es, bool mixed_src);
+
+// row statistics / LayerNorm fold: unsplit tiles of the 2-blocks-per-CU kernel with >= 64 rows;
+// GEGLU on 128x128 (the register epilogue needs a wave N extent of 32k)
 Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
+  Plan pl = make_plan_base(q, M, es, mixed_src);
+  if (q->row_stats || q->ln_rows) {
+    pl.ksplit = 1;
+    pl.stages = 2;
+    if (q->out_layout == LDM_OUT_GEGLU) { pl.bm = 128; pl.bn = 128; }
+    else if (pl.bm == 256 || pl.bm < 64) { pl.bm = 128; pl.bn = 160; }
+  }
+  return pl;
+}
+
+Plan make_plan_base(const ldm_conv_params* q, int M, int es, bool mixed_src) {
   Plan pl;
   const int bk = 128 / es;
   const int nk = q->kpad / bk;
@@ -1780,6 +1873,19 @@ int validate(const ldm_conv_params* q, int* es_out) {
   const int64_t M64 = (int64_t)q->batch * q->h_out * q->w_out;
   if (q->gn_partial && (M64 % 64 || (q->h_out * q->w_out) % 64 || q->out_layout != LDM_OUT_NHWC)) return LDM_ERR_ARG;
   if (q->gn_partial && (q->gn_unit < 0 || (q->gn_unit > 0 && q->n % q->gn_unit) || q->gn_slots < 0)) return LDM_ERR_ARG;
+  if (q->row_stats || q->ln_rows) {
+    // the row statistics and the LayerNorm fold live in the bf16 1x1 epilogues (staged NHWC /
+    // register GEGLU) of the unsplit 2-blocks-per-CU tiles
+    const auto a16 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; };
+    if (q->dtype != LDM_BF16 || q->ksize != 1 || q->temb || q->gn_partial || q->out_f32 || !a16(q->out) ||
+        !a16(q->residual) || !a16(q->bias) || q->n % 32)
+      return LDM_ERR_ARG;
+    if (q->row_stats && (q->out_layout != LDM_OUT_NHWC || !a16(q->row_stats))) return LDM_ERR_ARG;
+    if (q->ln_rows && (!q->ln_c1 || !a16(q->ln_c1) || (reinterpret_cast<uintptr_t>(q->ln_rows) & 7) ||
+                       q->ln_inv_k <= 0.f || (q->out_layout != LDM_OUT_NHWC && q->out_layout != LDM_OUT_GEGLU)))
+      return LDM_ERR_ARG;
+    if (!g_epi_pre && q->out_layout == LDM_OUT_NHWC) return LDM_ERR_ARG;
+  }
   const int64_t a0_bytes = (int64_t)q->batch * q->h_in * q->w_in * q->c0 * es;
   const int64_t a1_bytes = (int64_t)q->batch * q->h_in * q->w_in * q->c1 * es;
   const int64_t w_bytes = (int64_t)q->n * q->kpad * es;
@@ -1878,6 +1984,11 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.gn_unit = q->gn_unit > 0 ? q->gn_unit : 1;
   a.gn_slots = q->gn_slots > 0 ? q->gn_slots : 1;
   a.epi_pre = g_epi_pre;
+  a.row_stats = q->row_stats;
+  a.ln_rows = q->ln_rows;
+  a.ln_c1 = q->ln_c1;
+  a.ln_inv_k = q->ln_inv_k;
+  a.ln_eps = q->ln_eps;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (use_halo) return launch_halo(a, s);
   if (pl.bm == 256) return launch_big(a, s);

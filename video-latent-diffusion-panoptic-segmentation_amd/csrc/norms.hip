@@ -20,6 +20,12 @@ namespace {
 
 constexpr int GN_MAXC = 2560;        // channels per GroupNorm (the UNet's largest concat)
 constexpr int GN_STATS_SLOTS = 4;    // accumulator copies written by the fallback statistics kernel
+#ifndef GN_TARGET_BLOCKS
+#define GN_TARGET_BLOCKS 1024        // apply grid size (ablation builds vary it)
+#endif
+#ifndef GN_UNR
+#define GN_UNR 8                     // rows in flight per apply thread
+#endif
 
 // fallback statistics (no producer accumulators): grid (row blocks, batch); a block sums its
 // rows for every channel (column passes of <= 256 vectors, RB rows in parallel, fp32 over the
@@ -84,7 +90,7 @@ __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x0, const 
                                                 const float* __restrict__ gamma, const float* __restrict__ beta,
                                                 int act, T* __restrict__ out, float2* __restrict__ save) {
   constexpr int EPC = 16 / sizeof(T);
-  constexpr int UNR = 8;
+  constexpr int UNR = GN_UNR;
   extern __shared__ double2 ured[];
   __shared__ float2 gst[64];
   const int C = c0 + c1, V = C / EPC, cpg = C / groups;
@@ -314,7 +320,7 @@ int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw,
   const int ncol = (V + 255) / 256;
   const int bx = (V + ncol - 1) / ncol;
   const int rb = std::max(1, 256 / bx);
-  const int per_b = std::max(1, std::min((hw + rb - 1) / rb, (1024 + batch - 1) / batch));
+  const int per_b = std::max(1, std::min((hw + rb - 1) / rb, (GN_TARGET_BLOCKS + batch - 1) / batch));
   const int rpb = (hw + per_b - 1) / per_b;
   const int nb = (hw + rpb - 1) / rpb;
   const dim3 grid(nb, batch), block(bx, rb);

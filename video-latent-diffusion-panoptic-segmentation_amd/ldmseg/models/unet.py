@@ -411,6 +411,14 @@ class UNet(nn.Module):
                      heads=a1.heads, dim_head=a1.dim_head,
                      ff1=K.PackedConv(tb.ff.net[0].proj.weight, tb.ff.net[0].proj.bias, dt, geglu=True),
                      ff2=K.PackedConv(tb.ff.net[2].weight, tb.ff.net[2].bias, dt), attn2=None)
+            if dt == torch.bfloat16:
+                # norm1 -> QKV and norm3 -> ff.net.0 as single GEMMs on the raw rows (the producers,
+                # proj_in and to_out, sum each row's statistics in their epilogues)
+                d["qkv_ln"] = K.packed_ln_fold(torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight]), None,
+                                               tb.norm1.weight, tb.norm1.bias, dt)
+                d["ff1_ln"] = K.packed_ln_fold(tb.ff.net[0].proj.weight, tb.ff.net[0].proj.bias, tb.norm3.weight,
+                                               tb.norm3.bias, dt, geglu=True)
+                d["ln_eps"] = (tb.norm1.eps, tb.norm3.eps)
             if tb.attn2 is not None:
                 a2 = tb.attn2
                 d["attn2"] = dict(ln2=(f32(tb.norm2.weight), f32(tb.norm2.bias)),
@@ -492,19 +500,36 @@ class UNet(nn.Module):
             res = x0
         return K.conv2d(p["c2"], h, B, H, W, residual=res, gn_stats=True)
 
+    @property
+    def ln_fold(self):
+        return getattr(self, "_ln_fold", True)
+
+    def set_ln_fold(self, enabled=True):
+        """bf16 inference: fold norm1 / norm3 into the QKV / ff.net.0 GEMMs (default on); off runs
+        the separate LayerNorm kernels (A/B, and the form the training path differentiates)."""
+        self._ln_fold = bool(enabled)
+
     def _transformer(self, P, t, x, B, H, W, ehs):
         p = P[id(t)]
         C = x.shape[-1]
         N = H * W
         h = K.group_norm(x, B, N, t.groups, *p["norm"], 1e-6)
-        h = K.linear(p["proj_in"], h)                                    # [B, N, C]
-        n = K.layer_norm(h, *p["ln1"], 1e-5)
-        qkv = K.linear(p["qkv"], n)                                      # [B, N, 3C]
+        cross = p["attn2"] is not None and ehs is not None
+        if self.ln_fold and "qkv_ln" in p:
+            rs1 = K.zeroed_f32(2 * B * N, x.device)
+            rs3 = None if cross else K.zeroed_f32(2 * B * N, x.device)
+            h = K.linear(p["proj_in"], h, row_stats=rs1)                 # [B, N, C] + row (sum, sumsq)
+            qkv = K.linear(p["qkv_ln"], h, ln=(rs1, p["ln_eps"][0]))      # = to_qkv(norm1(h))
+        else:
+            rs3 = None
+            h = K.linear(p["proj_in"], h)                                # [B, N, C]
+            n = K.layer_norm(h, *p["ln1"], 1e-5)
+            qkv = K.linear(p["qkv"], n)                                  # [B, N, 3C]
         heads, dh = p["heads"], p["dim_head"]
         a = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, dh, N, N, 3 * C, 3 * C, 3 * C,
                         fp8=self.attention_fp8 and qkv.dtype == torch.bfloat16)
-        h = K.linear(p["out1"], a, residual=h, out=h)
-        if p["attn2"] is not None and ehs is not None:
+        h = K.linear(p["out1"], a, residual=h, out=h, row_stats=rs3)
+        if cross:
             q2 = p["attn2"]
             n = K.layer_norm(h, *q2["ln2"], 1e-5)
             q = K.linear(q2["q"], n)
@@ -513,8 +538,11 @@ class UNet(nn.Module):
             L = e.shape[1]
             a = K.attention(q, kv, kv[..., C:], B, heads, dh, N, L, C, 2 * C, 2 * C)
             h = K.linear(q2["out"], a, residual=h, out=h)
-        n = K.layer_norm(h, *p["ln3"], 1e-5)
-        f = K.linear(p["ff1"], n, out_layout=K.OUT_GEGLU)                # [B, N, 4C]
+        if rs3 is not None:
+            f = K.linear(p["ff1_ln"], h, out_layout=K.OUT_GEGLU, ln=(rs3, p["ln_eps"][1]))   # ff.net.0(norm3(h))
+        else:
+            n = K.layer_norm(h, *p["ln3"], 1e-5)
+            f = K.linear(p["ff1"], n, out_layout=K.OUT_GEGLU)            # [B, N, 4C]
         h = K.linear(p["ff2"], f, residual=h, out=h)
         return K.conv2d(p["proj_out"], h, B, H, W, residual=x, gn_stats=True)
 

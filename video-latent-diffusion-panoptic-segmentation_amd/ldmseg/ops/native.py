@@ -34,7 +34,8 @@ class ConvParams(ctypes.Structure):
                 ("h_out", _i), ("w_out", _i), ("ksize", _i), ("stride", _i), ("upsample", _i), ("w", _vp),
                 ("n", _i), ("kpad", _i), ("bias", _vp), ("temb", _vp), ("temb_stride", _i), ("residual", _vp),
                 ("out", _vp), ("out_layout", _i), ("act", _i), ("dtype", _i), ("out_f32", _i),
-                ("workspace", _vp), ("workspace_bytes", _i64), ("gn_partial", _vp), ("pad_mode", _i), ("gn_unit", _i), ("gn_slots", _i)]
+                ("workspace", _vp), ("workspace_bytes", _i64), ("gn_partial", _vp), ("pad_mode", _i), ("gn_unit", _i), ("gn_slots", _i),
+                ("row_stats", _vp), ("ln_rows", _vp), ("ln_c1", _vp), ("ln_inv_k", _f), ("ln_eps", _f)]
 
 
 class AttnParams(ctypes.Structure):
@@ -294,6 +295,20 @@ class PackedConv:
         self.shuffle2 = shuffle2 or convt4
 
 
+def packed_ln_fold(weight, bias, gamma, beta, dtype, geglu=False):
+    """Linear(LayerNorm(x)) as one GEMM on the raw rows x (ldm_conv_params ln_rows): the packed
+    weight is W' = W diag(gamma), the bias W beta + b, and ``ln_c1`` the column sums of the
+    packed (rounded) W', so that rstd (x W'^T - mean c1) cancels the mean exactly as packed."""
+    w = weight.detach().float()
+    wf = w * gamma.detach().float()[None, :]
+    b = w @ beta.detach().float()
+    if bias is not None:
+        b = b + bias.detach().float()
+    pc = PackedConv(wf, b, dtype, geglu=geglu)
+    pc.ln_c1 = pc.w.float().sum(1).contiguous()
+    return pc
+
+
 def packed_rows(t, bias=None):
     """Wrap a contiguous [n][k] activation tensor (k % 64 == 0) as the B operand of a 1x1
     ldm_conv2d without copying: out[m, j] = sum_k A[m, k] * t[j, k] (+ bias[j])."""
@@ -353,6 +368,12 @@ def gn_arena(key, device):
         _gn_arena_sizes[key] = max(need, st["used"])
 
 
+def zeroed_f32(count, device):
+    """A zeroed fp32 tensor of ``count`` (even) elements, from the enclosing gn_arena if any
+    (LayerNorm row statistics share the GroupNorm accumulators' one memset)."""
+    return _gn_accumulators(1, 1, (count + 3) // 4, device).view(torch.float32).view(-1)[:count]
+
+
 def _gn_accumulators(batch, slots, n, device):
     """Zeroed fp64 [batch, slots, n, 2] accumulators (n = units), from the enclosing gn_arena if any."""
     cnt = batch * slots * n * 2                   # even -> every slice stays 16-B aligned
@@ -369,12 +390,17 @@ def _gn_accumulators(batch, slots, n, device):
 
 
 def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False, temb=None, temb_stride=0,
-           residual=None, out=None, out_layout=OUT_NHWC, act=ACT_NONE, out_dtype=None, gn_stats=False, pad_mode=0):
+           residual=None, out=None, out_layout=OUT_NHWC, act=ACT_NONE, out_dtype=None, gn_stats=False, pad_mode=0,
+           row_stats=None, ln=None):
     """Run ldm_conv2d.  x0/x1: NHWC [batch, h, w, c] (any contiguous view with that numel).
 
     gn_stats=True also has the epilogue sum the per-(batch, channel) (sum, sumsq) of the output
     into fp64 accumulators (from the enclosing gn_arena when there is one); they are attached to
-    the returned tensor and consumed by group_norm()."""
+    the returned tensor and consumed by group_norm().
+
+    row_stats: a zeroed fp32 [M, 2] tensor the epilogue adds each output row's (sum, sumsq) to.
+    ln = (rows, eps): x0's rows are LayerNorm'd inside the GEMM (pc from packed_ln_fold, rows =
+    the producer's row_stats)."""
     lib = load_library()
     _gpu(x0, x1, pc.w, temb, residual, out)
     c0 = x0.numel() // (batch * h * w)
@@ -424,10 +450,22 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
     if gn_stats and out_layout == OUT_NHWC and M % 64 == 0 and (ho * wo) % 64 == 0:
         unit, slots = gn_unit_for(n), gn_slots_for(ho * wo)
         part = _gn_accumulators(batch, slots, n // unit, x0.device)
+    ln_rows, ln_c1, ln_inv_k, ln_eps = None, None, 0.0, 0.0
+    if row_stats is not None and (row_stats.dtype != torch.float32 or row_stats.numel() != 2 * M
+                                  or not row_stats.is_contiguous()):
+        raise ValueError("row_stats must be a contiguous fp32 [M, 2] tensor")
+    if ln is not None:
+        ln_rows, eps = ln
+        if getattr(pc, "ln_c1", None) is None:
+            raise ValueError("ln needs a packed_ln_fold weight")
+        if ln_rows.dtype != torch.float32 or ln_rows.numel() != 2 * M or not ln_rows.is_contiguous():
+            raise ValueError("ln rows must be a contiguous fp32 [M, 2] tensor")
+        ln_c1, ln_inv_k, ln_eps = pc.ln_c1, 1.0 / (c0 + c1), float(eps)
     p = ConvParams(_ptr(x0), _ptr(x1), c0, c1, batch, h, w, ho, wo, pc.ksize, stride, int(upsample), _ptr(pc.w),
                    n, pc.kpad, _ptr(pc.bias), _ptr(temb), temb_stride, _ptr(residual), _ptr(out), out_layout, act,
                    dtype_code(pc.dtype), int(odt == torch.float32 and pc.dtype != torch.float32), None, 0,
-                   _ptr(part), int(pad_mode), unit, slots)
+                   _ptr(part), int(pad_mode), unit, slots, _ptr(row_stats), _ptr(ln_rows), _ptr(ln_c1),
+                   float(ln_inv_k), float(ln_eps))
     ws_bytes = int(lib.ldm_conv2d_workspace_bytes(ctypes.byref(p)))
     if ws_bytes:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x0.device)
