@@ -121,6 +121,10 @@ void ldm_conv2d_set_raster_group(int group_m);
 /* Tuning hook: the halo-tiled 3x3 kernel (bf16, stride 1, 64-channel-aligned sources, output
  * width 64 or 32): 0 = planner's choice, 1 = never, 2 = whenever legal. */
 void ldm_conv2d_set_halo(int mode);
+/* Tuning hook: the A-register-stationary bf16 1x1 GEMM (K = 320, N a multiple of 160, NHWC or
+ * GEGLU, no time embedding / GroupNorm partials): 0 = planner's choice (the 64x64 UNet level),
+ * 1 = never, 2 = whenever legal. */
+void ldm_conv2d_set_ars(int mode);
 /* Tuning hook: bf16 NHWC epilogue of the 2-blocks-per-CU tiles — 0 = bias / time embedding /
  * activation applied from the accumulators and the tile staged once as bf16 (default),
  * 1 = fp32 staging in row halves (the round-1 form). */

@@ -171,6 +171,8 @@ def main():
     ap.add_argument("--groups", nargs="*", type=int, default=[8], help="conv tile-raster groups to compare")
     ap.add_argument("--lib", default=None, help="load this library build instead (e.g. exp/libabl1.so)")
     ap.add_argument("--epi", type=int, default=0, help="conv epilogue mode (ldm_conv2d_set_epilogue)")
+    ap.add_argument("--ars", nargs="*", type=int, default=[0],
+                    help="short-K 1x1 GEMM modes to compare (ldm_conv2d_set_ars: 0 planner, 1 never, 2 when legal)")
     a = ap.parse_args()
     if a.lib:
         K.load_library(os.path.abspath(a.lib))
@@ -183,17 +185,20 @@ def main():
             continue
         for pl in a.plans:
             for gm in a.groups:
-                run, fl, nb = CASES[n]()
-                f = [0, 0, 1, 0] if pl == "auto" else [int(v) for v in pl.split(",")] + [0]
-                bm, bn, ks, st = f[:4]
+                for am in a.ars:
+                    run, fl, nb = CASES[n]()
+                    f = [0, 0, 1, 0] if pl == "auto" else [int(v) for v in pl.split(",")] + [0]
+                    bm, bn, ks, st = f[:4]
 
-                def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm):
-                    K.force_conv_plan(bm, bn, ks)
-                    K.force_conv_stages(st)
-                    K.set_conv_raster_group(gm)
-                    return run()
-                name = n if pl == "auto" else f"{n}@{pl}"
-                built[name if len(a.groups) == 1 else f"{name}/g{gm}"] = (run_pl, fl, nb)
+                    def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm, am=am):
+                        K.force_conv_plan(bm, bn, ks)
+                        K.force_conv_stages(st)
+                        K.set_conv_raster_group(gm)
+                        K.set_conv_ars(am)
+                        return run()
+                    name = n if pl == "auto" else f"{n}@{pl}"
+                    name = name if len(a.groups) == 1 else f"{name}/g{gm}"
+                    built[name if len(a.ars) == 1 else f"{name}/ars{am}"] = (run_pl, fl, nb)
     for n, (run, _, _) in built.items():
         run()
     torch.cuda.synchronize()

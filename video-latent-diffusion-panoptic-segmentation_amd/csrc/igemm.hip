@@ -1911,6 +1911,8 @@ bool use_halo_plan(const ldm_conv_params* q, int es, bool mixed) {
   return q->n % halo::BN == 0 && (q->w_out == 64 || (q->w_out == 32 && q->c0 + q->c1 <= 960));
 }
 
+#include "gemm_ars.h"
+
 }  // namespace
 
 extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
@@ -1926,6 +1928,7 @@ extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
 int g_group_m = 8;
 extern "C" void ldm_conv2d_set_raster_group(int g) { g_group_m = g >= 1 ? g : 8; }
 extern "C" void ldm_conv2d_set_halo(int mode) { g_halo_mode = (mode == 1 || mode == 2) ? mode : 0; }
+extern "C" void ldm_conv2d_set_ars(int mode) { g_ars_mode = (mode >= 1 && mode <= 3) ? mode : 0; }
 extern "C" void ldm_conv2d_set_epilogue(int mode) { g_epi_pre = mode == 1 ? 0 : 1; }
 extern "C" void ldm_conv2d_force_stages(int stages) {
   g_force_stages = (stages == 1 || stages == 3 || stages == 4) ? stages : 0;   // 1: register-staged operands
@@ -1936,7 +1939,7 @@ extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   if (validate(q, &es) != LDM_OK) return 0;
   const int M = q->batch * q->h_out * q->w_out;
   const bool mixed = is_mixed(q, es);
-  if (use_halo_plan(q, es, mixed)) return 0;
+  if (use_halo_plan(q, es, mixed) || use_ars(q, es, mixed, M)) return 0;
   const Plan pl = make_plan(q, M, es, mixed);
   return pl.ksplit > 1 ? (size_t)pl.ksplit * M * q->n * sizeof(float) : 0;
 }
@@ -1950,7 +1953,8 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   const int M = q->batch * q->h_out * q->w_out;
   const bool mixed = is_mixed(q, es);
   const bool use_halo = use_halo_plan(q, es, mixed);
-  const Plan pl = use_halo ? Plan{0, 0, 1} : make_plan(q, M, es, mixed);
+  const bool ars = !use_halo && use_ars(q, es, mixed, M);
+  const Plan pl = (use_halo || ars) ? Plan{0, 0, 1} : make_plan(q, M, es, mixed);
   if (pl.ksplit > 1) {
     const size_t need = (size_t)pl.ksplit * M * q->n * sizeof(float);
     if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;
@@ -1991,6 +1995,7 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.ln_eps = q->ln_eps;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (use_halo) return launch_halo(a, s);
+  if (ars) return launch_ars(a, s);
   if (pl.bm == 256) return launch_big(a, s);
   const int stages = g_force_stages ? g_force_stages : pl.stages;
   return q->dtype == LDM_BF16 ? launch_t<bf16_t>(a, s, pl.bm, pl.bn, stages) : launch_t<float>(a, s, pl.bm, pl.bn);

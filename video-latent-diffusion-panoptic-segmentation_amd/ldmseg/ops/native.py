@@ -65,6 +65,7 @@ EXPORTS = {
     "ldm_conv2d_force_stages": (None, [_i]),
     "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_conv2d_set_halo": (None, [_i]),
+    "ldm_conv2d_set_ars": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp]),
@@ -527,6 +528,11 @@ def set_conv_raster_group(group_m=8):
 def set_conv_halo(mode=0):
     """Tuning hook: halo-tiled 3x3 kernel — 0 planner, 1 never, 2 whenever legal."""
     load_library().ldm_conv2d_set_halo(int(mode))
+
+
+def set_conv_ars(mode=0):
+    """Tuning hook: A-register-stationary short-K 1x1 GEMM — 0 planner, 1 never, 2 whenever legal."""
+    load_library().ldm_conv2d_set_ars(int(mode))
 
 
 def set_conv_epilogue(mode=0):
