@@ -125,6 +125,9 @@ void ldm_conv2d_set_halo(int mode);
  * GEGLU, no time embedding / GroupNorm partials): 0 = planner's choice (the 64x64 UNet level),
  * 1 = never, 2 = whenever legal. */
 void ldm_conv2d_set_ars(int mode);
+/* Tuning hook: column width of the split-K reduction kernel's 64-row tiles — 0 = planner's choice
+ * (64 when 128-wide tiles give fewer than 512 blocks), 64 or 128 forced. */
+void ldm_conv2d_set_splitk_cols(int cols);
 /* Tuning hook: bf16 NHWC epilogue of the 2-blocks-per-CU tiles — 0 = bias / time embedding /
  * activation applied from the accumulators and the tile staged once as bf16 (default),
  * 1 = fp32 staging in row halves (the round-1 form). */

@@ -30,6 +30,10 @@ def plan():
     yield set_plan
     K.force_conv_plan(0, 0, 1)
     K.force_conv_stages(0)
+    K.set_conv_splitk_cols(0)
+
+
+SKC = [64, 128]     # split-K reduction tile widths (ldm_conv2d_set_splitk_cols; both forced)
 
 
 PLANS = [(256, 160, 1, 0), (256, 160, 3, 0), (128, 160, 1, 0), (128, 160, 1, 3), (128, 160, 3, 4), (64, 160, 2, 0),
@@ -46,9 +50,12 @@ SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("skc", SKC)
 @pytest.mark.parametrize("pl", PLANS, ids=[f"{a}x{b}_k{c}_s{d}" for a, b, c, d in PLANS])
 @pytest.mark.parametrize("case", SHAPES, ids=[s[0] for s in SHAPES])
-def test_conv_plan(case, pl, plan):
+def test_conv_plan(case, pl, skc, plan):
+    if pl[2] == 1 and skc != SKC[0]:
+        pytest.skip("unsplit plan: no split-K reduction")
     name, B, c0, c1, H, W, Co, k, s, up = case
     torch.manual_seed(3)
     x = torch.randn(B, c0 + c1, H, W)
@@ -64,13 +71,15 @@ def test_conv_plan(case, pl, plan):
     x0 = xn[..., :c0].contiguous()
     x1 = xn[..., c0:].contiguous() if c1 else None
     plan(*pl)
+    K.set_conv_splitk_cols(skc)
     out = K.conv2d(pc, x0, B, H, W, x1=x1, stride=s, upsample=up, temb=temb.to(DEV), temb_stride=Co,
                    residual=resid.permute(0, 2, 3, 1).contiguous().to(DEV, BF), act=K.ACT_SILU)
     assert rel_err(out.permute(0, 3, 1, 2), ref) < 2e-2
 
 
+@pytest.mark.parametrize("skc", SKC)
 @pytest.mark.parametrize("pl", PLANS, ids=[f"{a}x{b}_k{c}_s{d}" for a, b, c, d in PLANS])
-def test_plan_groupnorm_stats(pl, plan):
+def test_plan_groupnorm_stats(pl, skc, plan):
     """Epilogue GroupNorm partials (two 128-row halves in the large kernel, split-K reduce)."""
     B, H, C, Co, G = 2, 16, 192, 320, 32
     torch.manual_seed(4)
@@ -80,6 +89,7 @@ def test_plan_groupnorm_stats(pl, plan):
     y_ref = F.conv2d(x, w, b, padding=1)
     pc = K.PackedConv(w.to(DEV), b.to(DEV), BF)
     plan(*pl)
+    K.set_conv_splitk_cols(skc)
     y = K.conv2d(pc, x.permute(0, 2, 3, 1).contiguous().to(DEV, BF), B, H, H, gn_stats=True)
     assert K.gn_stats_of(y) is not None
     gam, bet = torch.randn(Co), torch.randn(Co)

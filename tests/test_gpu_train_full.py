@@ -116,16 +116,21 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_ddp_world2_equals_single_process_on_concatenated_batch(tmp_path):
+def _inputs(tmp_path):
     g = torch.Generator().manual_seed(4)
     I, B, L = 2, 4, 16
     d = {"latents": torch.randn(I, B, 4, L, L, generator=g), "rgb": torch.randn(I, B, 4, L, L, generator=g),
          "mask": (torch.rand(I, B, L, L, generator=g) > 0.1).float(), "noise": torch.randn(I, B, 4, L, L, generator=g),
          "t": torch.randint(0, 1000, (I, B), generator=g)}
     torch.save(d, tmp_path / "in.pt")
+    return d, I
+
+
+def _run_world2(tmp_path, tag, *extra):
+    """Two ranks of tests/ddp_train_worker.py on this GPU (gloo); returns their saved records."""
     env = dict(os.environ, WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "ddp_train_worker.py"), str(tmp_path / "in.pt"),
-                               str(tmp_path / "rank")], env=dict(env, RANK=str(r)))
+                               str(tmp_path / tag), *extra], env=dict(env, RANK=str(r)))
              for r in range(2)]
     try:
         rcs = [p.wait(timeout=100) for p in procs]
@@ -134,7 +139,12 @@ def test_ddp_world2_equals_single_process_on_concatenated_batch(tmp_path):
             if p.poll() is None:
                 p.kill()
     assert rcs == [0, 0], rcs
-    r0, r1 = (torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(2))
+    return [torch.load(tmp_path / f"{tag}{r}.pt", weights_only=True) for r in range(2)]
+
+
+def test_ddp_world2_equals_single_process_on_concatenated_batch(tmp_path):
+    d, I = _inputs(tmp_path)
+    r0, r1 = _run_world2(tmp_path, "rank")
     assert r0["buckets"] > 10
     assert torch.equal(r0["init"], r1["init"])                      # the rank-0 broadcast ...
     assert torch.equal(r0["frozen"], r1["frozen"])                  # ... of the frozen time_embedding too
@@ -159,3 +169,25 @@ def test_ddp_world2_equals_single_process_on_concatenated_batch(tmp_path):
         dm = r0["final"][o:o + k] - r0["init"][o:o + k]
         worst.append(((dm - dref).norm() / dref.norm().clamp_min(1e-30)).item())
     assert max(worst) < 1e-2, sorted(worst)[-5:]
+
+
+def test_zero1_world2_matches_unsharded_ddp(tmp_path):
+    """ZeRO stage 1 (optim.py:71-78, train_diffusion.sh:27): each rank keeps the AdamW moments of
+    half the flat buffer, updates that half and all-gathers it.  The optimizer alone (identical
+    state and gradients) equals the unsharded run bit for bit, weights and consolidated state;
+    two full training iterations agree to the run-to-run tolerance of the backward's atomics."""
+    _inputs(tmp_path)
+    z0, z1 = _run_world2(tmp_path, "zero", "zero")
+    r0, _ = _run_world2(tmp_path, "plain")
+    n = r0["final"].numel()
+    (a0, b0), (a1, b1) = z0["shard"].tolist(), z1["shard"].tolist()
+    assert a0 == 0 and b0 == a1 and b1 == n                         # disjoint shards covering the buffer
+    assert z0["moment_numel"] == b0 - a0 and z1["moment_numel"] == b1 - a1 and r0["moment_numel"] == n
+    assert torch.equal(z0["final"], z1["final"]) and torch.equal(z0["opt_final"], z1["opt_final"])
+    assert torch.equal(z0["opt_final"], r0["opt_final"])
+    assert torch.equal(z0["opt_moments"], r0["opt_moments"]) and torch.equal(z1["opt_moments"], r0["opt_moments"])
+    assert torch.equal(z0["moments"], z1["moments"])
+    dz, dp = z0["final"] - z0["init"], r0["final"] - r0["init"]
+    assert torch.equal(z0["init"], r0["init"])
+    assert ((dz - dp).norm() / dp.norm()).item() < 1e-2
+    assert ((z0["moments"] - r0["moments"]).norm() / r0["moments"].norm()).item() < 1e-3

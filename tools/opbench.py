@@ -111,6 +111,9 @@ CASES = {
     "conv3_l2_up_2560": lambda: conv_case(8, 16, 16, 2560, 1280, c1=1280, residual=True, stats=True),
     "gemm_proj_1280_l2": lambda: conv_case(8, 16, 16, 1280, 1280, k=1, residual=True),
     "gemm_proj_1280_l3": lambda: conv_case(8, 8, 8, 1280, 1280, k=1, residual=True),
+    "gemm_short_l3_2560": lambda: conv_case(8, 8, 8, 2560, 1280, k=1, c1=1280, residual=True),
+    "gemm_short_l2_2560": lambda: conv_case(8, 16, 16, 2560, 1280, k=1, c1=1280, residual=True),
+    "gemm_short_l2_1920": lambda: conv_case(8, 16, 16, 1920, 1280, k=1, c1=640, residual=True),
     "gemm_qkv_1280": lambda: conv_case(8, 16, 16, 1280, 3840, k=1),
     "gemm_ff2_5120": lambda: conv_case(8, 16, 16, 5120, 1280, k=1, residual=True),
     "gemm_geglu_1280_l2": lambda: conv_case(8, 16, 16, 1280, 10240, k=1, geglu=True),
@@ -173,6 +176,8 @@ def main():
     ap.add_argument("--epi", type=int, default=0, help="conv epilogue mode (ldm_conv2d_set_epilogue)")
     ap.add_argument("--ars", nargs="*", type=int, default=[0],
                     help="short-K 1x1 GEMM modes to compare (ldm_conv2d_set_ars: 0 planner, 1 never, 2 when legal)")
+    ap.add_argument("--skcols", nargs="*", type=int, default=[0],
+                    help="split-K reduction tile widths to compare (ldm_conv2d_set_splitk_cols: 0 planner, 64, 128)")
     a = ap.parse_args()
     if a.lib:
         K.load_library(os.path.abspath(a.lib))
@@ -185,12 +190,13 @@ def main():
             continue
         for pl in a.plans:
             for gm in a.groups:
-                for am in a.ars:
+                for am, sk in [(x, y) for x in a.ars for y in a.skcols]:
                     run, fl, nb = CASES[n]()
                     f = [0, 0, 1, 0] if pl == "auto" else [int(v) for v in pl.split(",")] + [0]
                     bm, bn, ks, st = f[:4]
 
-                    def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm, am=am):
+                    def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm, am=am, sk=sk):
+                        K.set_conv_splitk_cols(sk)
                         K.force_conv_plan(bm, bn, ks)
                         K.force_conv_stages(st)
                         K.set_conv_raster_group(gm)
@@ -198,7 +204,8 @@ def main():
                         return run()
                     name = n if pl == "auto" else f"{n}@{pl}"
                     name = name if len(a.groups) == 1 else f"{name}/g{gm}"
-                    built[name if len(a.ars) == 1 else f"{name}/ars{am}"] = (run_pl, fl, nb)
+                    name = name if len(a.ars) == 1 else f"{name}/ars{am}"
+                    built[name if len(a.skcols) == 1 else f"{name}/skc{sk}"] = (run_pl, fl, nb)
     for n, (run, _, _) in built.items():
         run()
     torch.cuda.synchronize()

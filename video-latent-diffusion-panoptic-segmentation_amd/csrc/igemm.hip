@@ -1144,30 +1144,33 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   }
 }
 
-// Split-K reduction + full epilogue: one block per 64-row x 128-channel tile.
-template <typename T>
+// Split-K reduction + full epilogue: one block per 64-row x COLS-channel tile (COLS 64 when
+// 128-wide tiles would leave the chip under-filled: the 8x8 / 16x16 levels have 80-320 of
+// them).  Per thread the loads of two splits are in flight before their adds.
+template <typename T, int COLS = 128>
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) {
-  constexpr int ROWS = 64, COLS = 128, PITCH = COLS + 4, RPQ = 256 / (COLS / 4);   // 8 rows per pass
-  __shared__ float stage[ROWS * PITCH];   // also the statistics scratch of either epilogue
-  static_assert(gn_red_floats<256, COLS, ROWS, 8>() <= ROWS * PITCH && gn_red_floats<256, COLS, ROWS, 4>() <= ROWS * PITCH,
-                "GN scratch exceeds the stage");
-  const int tiles_n = (p.n + 127) / 128;
+  constexpr int ROWS = 64, PITCH = COLS + 4, RPQ = 256 / (COLS / 4);   // 8 or 16 rows per pass
+  constexpr int NQ = ROWS / RPQ;
+  constexpr int RED = gn_red_floats<256, COLS, ROWS, 8>() > gn_red_floats<256, COLS, ROWS, 4>()
+                          ? gn_red_floats<256, COLS, ROWS, 8>() : gn_red_floats<256, COLS, ROWS, 4>();
+  constexpr int SF = ROWS * PITCH > RED ? ROWS * PITCH : RED;
+  __shared__ float stage[SF];   // also the statistics scratch of either epilogue
+  const int tiles_n = (p.n + COLS - 1) / COLS;
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
-  const int m0 = tm * 64, n0 = tn * 128;
+  const int m0 = tm * 64, n0 = tn * COLS;
   const int64_t slab = (int64_t)p.M * p.n;
-  // phase A: sum the slabs into LDS; per split, the 8 rows of a thread are loaded together
+  // phase A: sum the slabs into LDS; the rows of a thread for two splits are loaded together
   {
     const int c4 = threadIdx.x % (COLS / 4), r0 = threadIdx.x / (COLS / 4);
     const int n = n0 + 4 * c4;
     const bool vec = n + 3 < p.n;
-    float4 acc[ROWS / RPQ];
+    float4 acc[NQ];
 #pragma unroll
-    for (int q = 0; q < ROWS / RPQ; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int sp = 0; sp < p.ksplit; ++sp) {
+    for (int q = 0; q < NQ; ++q) acc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto load = [&](int sp, float4* x) {
       const float* src = p.partial + sp * slab;
-      float4 x[ROWS / RPQ];
 #pragma unroll
-      for (int q = 0; q < ROWS / RPQ; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         const int m = m0 + r0 + q * RPQ;
         x[q] = make_float4(0.f, 0.f, 0.f, 0.f);
         if (m < p.M && n < p.n) {
@@ -1181,13 +1184,28 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) 
           }
         }
       }
+    };
+    int sp = 0;
+    for (; sp + 1 < p.ksplit; sp += 2) {
+      float4 x[NQ], y[NQ];
+      load(sp, x);
+      load(sp + 1, y);
 #pragma unroll
-      for (int q = 0; q < ROWS / RPQ; ++q) {
+      for (int q = 0; q < NQ; ++q) {
+        acc[q].x += x[q].x; acc[q].y += x[q].y; acc[q].z += x[q].z; acc[q].w += x[q].w;
+        acc[q].x += y[q].x; acc[q].y += y[q].y; acc[q].z += y[q].z; acc[q].w += y[q].w;
+      }
+    }
+    if (sp < p.ksplit) {
+      float4 x[NQ];
+      load(sp, x);
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
         acc[q].x += x[q].x; acc[q].y += x[q].y; acc[q].z += x[q].z; acc[q].w += x[q].w;
       }
     }
 #pragma unroll
-    for (int q = 0; q < ROWS / RPQ; ++q)
+    for (int q = 0; q < NQ; ++q)
       *reinterpret_cast<float4*>(stage + (r0 + q * RPQ) * PITCH + 4 * c4) = acc[q];
   }
   __syncthreads();
@@ -1652,6 +1670,17 @@ int launch_halo(ConvArgs a, hipStream_t s) {
   return LDM_OK;
 }
 
+int g_splitk_cols = 0;    // tuning hook (ldm_conv2d_set_splitk_cols): 0 planner, 64 / 128 forced
+
+template <typename T>
+void launch_splitk_epilogue(const ConvArgs& a, hipStream_t s) {
+  const int mt = (a.M + 63) / 64;
+  const int b128 = mt * ((a.n + 127) / 128);
+  const bool narrow = g_splitk_cols == 64 || (g_splitk_cols == 0 && b128 < 512);
+  if (narrow) hipLaunchKernelGGL((splitk_epilogue_kernel<T, 64>), dim3(mt * ((a.n + 63) / 64)), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((splitk_epilogue_kernel<T, 128>), dim3(b128), dim3(256), 0, s, a);
+}
+
 int g_force_stages = 0;   // tuning hook: 1 register-staged operands, 3 / 4 ring depth, 0 planner
 
 template <typename T, int BM, int BN, int NS = 2>
@@ -1664,11 +1693,7 @@ int launch_bm_bn(ConvArgs a, hipStream_t s) {
   else
     hipLaunchKernelGGL((igemm_kernel<T, BM, BN, true, NS>), dim3(a.nblk), dim3(256), 0, s, a);
   LDM_CHECK_LAUNCH();
-  if (a.ksplit > 1) {
-    const int blocks = ((a.M + 63) / 64) * ((a.n + 127) / 128);
-    hipLaunchKernelGGL((splitk_epilogue_kernel<T>), dim3(blocks), dim3(256), 0, s, a);
-    LDM_CHECK_LAUNCH();
-  }
+  if (a.ksplit > 1) launch_splitk_epilogue<T>(a, s);
   return LDM_OK;
 }
 
@@ -1704,11 +1729,7 @@ int launch_big(ConvArgs a, hipStream_t s) {
   else if (g_big_mode == 2) hipLaunchKernelGGL(igemm_big_kernel<2>, dim3(a.nblk), dim3(big::NT), 0, s, a);
   else hipLaunchKernelGGL(igemm_big_kernel<0>, dim3(a.nblk), dim3(big::NT), 0, s, a);
   LDM_CHECK_LAUNCH();
-  if (a.ksplit > 1) {
-    const int blocks = ((a.M + 63) / 64) * ((a.n + 127) / 128);
-    hipLaunchKernelGGL((splitk_epilogue_kernel<bf16_t>), dim3(blocks), dim3(256), 0, s, a);
-    LDM_CHECK_LAUNCH();
-  }
+  if (a.ksplit > 1) launch_splitk_epilogue<bf16_t>(a, s);
   return LDM_OK;
 }
 
@@ -1929,6 +1950,7 @@ int g_group_m = 8;
 extern "C" void ldm_conv2d_set_raster_group(int g) { g_group_m = g >= 1 ? g : 8; }
 extern "C" void ldm_conv2d_set_halo(int mode) { g_halo_mode = (mode == 1 || mode == 2) ? mode : 0; }
 extern "C" void ldm_conv2d_set_ars(int mode) { g_ars_mode = (mode >= 1 && mode <= 3) ? mode : 0; }
+extern "C" void ldm_conv2d_set_splitk_cols(int cols) { g_splitk_cols = (cols == 64 || cols == 128) ? cols : 0; }
 extern "C" void ldm_conv2d_set_epilogue(int mode) { g_epi_pre = mode == 1 ? 0 : 1; }
 extern "C" void ldm_conv2d_force_stages(int stages) {
   g_force_stages = (stages == 1 || stages == 3 || stages == 4) ? stages : 0;   // 1: register-staged operands

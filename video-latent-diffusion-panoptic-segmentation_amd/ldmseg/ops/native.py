@@ -66,6 +66,7 @@ EXPORTS = {
     "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_conv2d_set_halo": (None, [_i]),
     "ldm_conv2d_set_ars": (None, [_i]),
+    "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp]),
@@ -533,6 +534,11 @@ def set_conv_halo(mode=0):
 def set_conv_ars(mode=0):
     """Tuning hook: A-register-stationary short-K 1x1 GEMM — 0 planner, 1 never, 2 whenever legal."""
     load_library().ldm_conv2d_set_ars(int(mode))
+
+
+def set_conv_splitk_cols(cols=0):
+    """Tuning hook: split-K reduction tile width — 0 planner, 64 or 128 forced."""
+    load_library().ldm_conv2d_set_splitk_cols(int(cols))
 
 
 def set_conv_epilogue(mode=0):

@@ -19,6 +19,13 @@ the step.  With torch.distributed initialised, gradients are summed by bucketed 
 that start while the backward is still running (trainers/ddp.py); the loss gradient carries
 the 1/world factor so the sum is DDP's average.
 
+ZeRO stage 1 (``zero_redundancy=True``; optim.py:71-78 wraps AdamW in
+ZeroRedundancyOptimizer when ``optimizer_zero_redundancy`` is set, tools/scripts/
+train_diffusion.sh:27): the AdamW moments exist only for this rank's contiguous shard of the
+flat buffer; gradients are still all-reduced whole (DDP), the clip norm is taken over the whole
+reduced gradient, each rank updates its shard, and the shards are all-gathered back into every
+rank's parameters — the same arithmetic, element for element, as the unsharded step.
+
 Not native (raises): ohem_ratio < 1, rgb/cond noise levels > 0, inpainting masks,
 prob_train_on_pred > 0 — all off in base.yaml / train_diffusion.sh.
 """
@@ -74,7 +81,7 @@ def unet_backward_order(unet):
 class LDMTrainStep:
     def __init__(self, unet, scheduler, lr=1e-4, weight_decay=0.0, weight_decay_norm=0.0, betas=(0.9, 0.999),
                  eps=1e-8, clip_grad=3.0, lr_factor_func=None, self_condition=False, min_noise_level=0,
-                 compute_dtype=torch.bfloat16, bucket_mb=100, group=None, seed=None):
+                 compute_dtype=torch.bfloat16, bucket_mb=100, group=None, seed=None, zero_redundancy=False):
         self.unet, self.sched = unet, scheduler
         self.self_condition = self_condition
         self.min_noise_level = min_noise_level
@@ -101,9 +108,20 @@ class LDMTrainStep:
             wd = weight_decay_norm if id(p) in norm_ids else weight_decay
             self.seg_hp.append([o, o + p.numel(), plr, wd])
             self.seg_key.append((plr, wd if id(p) in norm_ids else None))
+        # ZeRO-1 shard [lo, hi) of the flat buffer (the whole buffer without it); shards are
+        # S elements (a multiple of 64) so the all-gather moves equal pieces
+        self.zero = bool(zero_redundancy) and self.world > 1
+        n = self.flat.numel
+        if self.zero:
+            self.rank = dist.get_rank(group)
+            self.shard_len = -(-n // (64 * self.world)) * 64
+            lo = min(self.rank * self.shard_len, n)
+            self.shard = (lo, min(lo + self.shard_len, n))
+        else:
+            self.shard = (0, n)
         self._upload_segments()
-        self.exp_avg = torch.zeros_like(self.flat.data)
-        self.exp_avg_sq = torch.zeros_like(self.flat.data)
+        self.exp_avg = torch.zeros(self.shard[1] - self.shard[0], dtype=torch.float32, device=dev)
+        self.exp_avg_sq = torch.zeros_like(self.exp_avg)
         self.step_count = 0
         # DistributedDataParallel(...) broadcasts rank 0's module state — every parameter, the
         # frozen time_embedding included, and every buffer — when it is constructed
@@ -125,9 +143,37 @@ class LDMTrainStep:
             for t in tensors:
                 dist.broadcast(t, self._src(), group=self.group)
 
+    def shard_segments(self):
+        """The AdamW segment records of this rank's shard: every segment that intersects
+        [lo, hi), clipped to it and re-based to lo (all of them without ZeRO)."""
+        lo, hi = self.shard
+        return [(max(s, lo) - lo, min(e, hi) - lo, lr, wd) for s, e, lr, wd in self.seg_hp if e > lo and s < hi]
+
     def _upload_segments(self):
-        recs = b"".join(struct.pack("<qqff", s, e, lr, wd) for s, e, lr, wd in self.seg_hp)
+        segs = self.shard_segments()
+        self.nseg = len(segs)
+        recs = b"".join(struct.pack("<qqff", s, e, lr, wd) for s, e, lr, wd in segs) or bytes(24)
         self.segs = torch.frombuffer(bytearray(recs), dtype=torch.uint8).to(self.flat.data.device)
+
+    def _full(self, shard_buf):
+        """The whole-buffer tensor of a sharded one (collective under ZeRO; the buffer itself
+        otherwise).  Gathered by an all-reduce of zero-padded copies when the backend is not
+        RCCL (gloo has no CUDA all-gather); x + 0 is exact."""
+        if not self.zero:
+            return shard_buf
+        S, w, r = self.shard_len, self.world, self.rank
+        buf = torch.zeros(S * w, dtype=shard_buf.dtype, device=shard_buf.device)
+        buf[r * S:r * S + shard_buf.numel()].copy_(shard_buf)
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(buf, buf[r * S:(r + 1) * S].clone(), group=self.group)
+        else:
+            dist.all_reduce(buf, group=self.group)
+        return buf[:self.flat.numel]
+
+    def _gather_parameters(self):
+        """ZeroRedundancyOptimizer.step's parameter sync: every rank's updated shard to all."""
+        lo, hi = self.shard
+        self.flat.data.copy_(self._full(self.flat.data[lo:hi]))
 
     def set_lr(self, lr):
         """update_scheduler (trainers_ldm_cond.py:783-790): the scheduled lr replaces EVERY
@@ -159,7 +205,10 @@ class LDMTrainStep:
         return d
 
     def state_dict(self):
-        """torch.optim.AdamW.state_dict() of the same optimizer (fp32 moments, ``step``)."""
+        """torch.optim.AdamW.state_dict() of the same optimizer (fp32 moments, ``step``).  Under
+        ZeRO this is collective (ZeroRedundancyOptimizer.consolidate_state_dict): every rank
+        returns the whole state."""
+        exp_avg, exp_avg_sq = self._full(self.exp_avg), self._full(self.exp_avg_sq)
         state, pgs, idx = {}, [], 0
         for _, ps in self.reference_param_groups():
             _, _, lr, wd = self.seg_hp[self.flat.index[id(ps[0])]]        # the group's current lr
@@ -167,8 +216,8 @@ class LDMTrainStep:
             for q in ps:
                 if self.step_count > 0:
                     state[idx] = {"step": torch.tensor(float(self.step_count)),
-                                  "exp_avg": self.flat.view_of(q, self.exp_avg).detach().clone(),
-                                  "exp_avg_sq": self.flat.view_of(q, self.exp_avg_sq).detach().clone()}
+                                  "exp_avg": self.flat.view_of(q, exp_avg).detach().clone(),
+                                  "exp_avg_sq": self.flat.view_of(q, exp_avg_sq).detach().clone()}
                 ids.append(idx)
                 idx += 1
             pgs.append({**self._group_defaults(lr, wd), "params": ids})
@@ -178,6 +227,8 @@ class LDMTrainStep:
         """Inverse of state_dict(); also accepts a reference run's AdamW state_dict when its
         parameter grouping matches (same lr factors / weight decays)."""
         groups = self.reference_param_groups()
+        exp_avg = torch.zeros_like(self.flat.data)          # whole-buffer moments, sharded below
+        exp_avg_sq = torch.zeros_like(self.flat.data)
         if len(groups) != len(sd["param_groups"]):
             raise ValueError(f"optimizer has {len(groups)} parameter groups, checkpoint {len(sd['param_groups'])}")
         steps = set()
@@ -189,32 +240,29 @@ class LDMTrainStep:
                 seg = self.seg_hp[self.flat.index[id(q)]]
                 seg[2], seg[3] = float(g["lr"]), float(g["weight_decay"])
                 if st is None:
-                    self.flat.view_of(q, self.exp_avg).zero_()
-                    self.flat.view_of(q, self.exp_avg_sq).zero_()
                     continue
                 if tuple(st["exp_avg"].shape) != tuple(q.shape):
                     raise ValueError("optimizer state shape differs from the parameter's")
-                self.flat.view_of(q, self.exp_avg).copy_(st["exp_avg"])
-                self.flat.view_of(q, self.exp_avg_sq).copy_(st["exp_avg_sq"])
+                self.flat.view_of(q, exp_avg).copy_(st["exp_avg"])
+                self.flat.view_of(q, exp_avg_sq).copy_(st["exp_avg_sq"])
                 steps.add(int(float(st["step"])))
         if len(steps) > 1:
             raise ValueError("per-parameter step counts differ; the fused AdamW keeps one count")
         self.step_count = steps.pop() if steps else 0
-        self._upload_segments()
         if self.world > 1:
             # collective: every rank resumes (trainers_ldm_cond.py:1879-1914 runs on all ranks);
             # rank 0's moments, step count and learning rates win, like its parameters at init
-            cnt = torch.tensor([float(self.step_count)], dtype=torch.float64, device=self.flat.data.device)
-            self._broadcast(self.exp_avg, self.exp_avg_sq, cnt, self.segs)
+            dev = self.flat.data.device
+            cnt = torch.tensor([float(self.step_count)], dtype=torch.float64, device=dev)
+            hp = torch.tensor([[s[2], s[3]] for s in self.seg_hp], dtype=torch.float32, device=dev)
+            self._broadcast(exp_avg, exp_avg_sq, cnt, hp)
             self.step_count = int(cnt.item())
-            self._download_segments()
-
-    def _download_segments(self):
-        import numpy as np
-        rec = np.frombuffer(self.segs.cpu().numpy().tobytes(), dtype=np.dtype([("s", "<i8"), ("e", "<i8"),
-                                                                                ("lr", "<f4"), ("wd", "<f4")]))
-        for seg, r in zip(self.seg_hp, rec):
-            seg[2], seg[3] = float(r["lr"]), float(r["wd"])
+            for seg, (lr, wd) in zip(self.seg_hp, hp.tolist()):
+                seg[2], seg[3] = lr, wd
+        lo, hi = self.shard
+        self.exp_avg.copy_(exp_avg[lo:hi])
+        self.exp_avg_sq.copy_(exp_avg_sq[lo:hi])
+        self._upload_segments()
 
     def broadcast_parameters(self):
         """Re-sync every rank's module state to rank 0's (collective), e.g. after a load on rank 0:
@@ -259,10 +307,19 @@ class LDMTrainStep:
                                      grad_scale=1.0 / (pred.numel() * self.world))
         graph.backward(dpred)
         self.bucketer.finish()
-        self.step_count += 1
-        K.sq_norm(self.flat.grad, out=self.sqsum)
-        K.adamw(self.flat.data, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.segs, len(self.seg_hp),
-                self.step_count, self.betas[0], self.betas[1], self.eps, sqsum=self.sqsum,
-                max_norm=self.clip_grad if self.clip_grad > 0 else 0.0)
-        u.invalidate_packed()
+        self.optimizer_step()
         return loss_sum / pred.numel()
+
+    def optimizer_step(self):
+        """clip_grad_norm_ + AdamW step over the (reduced) flat gradient: this rank's shard under
+        ZeRO, followed by the parameter all-gather."""
+        self.step_count += 1
+        K.sq_norm(self.flat.grad, out=self.sqsum)          # the whole reduced gradient (clip_grad_norm_)
+        lo, hi = self.shard
+        if self.nseg:
+            K.adamw(self.flat.data[lo:hi], self.flat.grad[lo:hi], self.exp_avg, self.exp_avg_sq, self.segs, self.nseg,
+                    self.step_count, self.betas[0], self.betas[1], self.eps, sqsum=self.sqsum,
+                    max_norm=self.clip_grad if self.clip_grad > 0 else 0.0)
+        if self.zero:
+            self._gather_parameters()
+        self.unet.invalidate_packed()
