@@ -1186,6 +1186,17 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) 
       }
     };
     int sp = 0;
+    for (; sp + 3 < p.ksplit; sp += 4) {
+      float4 x[4][NQ];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) load(sp + u, x[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          acc[q].x += x[u][q].x; acc[q].y += x[u][q].y; acc[q].z += x[u][q].z; acc[q].w += x[u][q].w;
+        }
+    }
     for (; sp + 1 < p.ksplit; sp += 2) {
       float4 x[NQ], y[NQ];
       load(sp, x);
