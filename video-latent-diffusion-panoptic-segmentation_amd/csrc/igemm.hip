@@ -1853,6 +1853,12 @@ Plan make_plan_base(const ldm_conv_params* q, int M, int es, bool mixed_src) {
     pl.ksplit = std::max(1, std::min(nk / 16, (512 + t64 - 1) / t64));
     return pl;
   }
+  // 1x1 over few rows with moderately deep K (the 8x8 level's [1280 || 1280] -> 1280 shortcut,
+  // nk 40): 64x64 tiles split 4 ways (27 -> 22 us; unsplit 64x64 leaves 160 blocks of 40 K tiles)
+  if (es == 2 && q->ksize == 1 && M <= 512 && nk >= 40 && split_ok) {
+    pl.bm = 64; pl.bn = 64; pl.ksplit = 4;
+    return pl;
+  }
   const int bn_small = q->n <= 32 ? 32 : (q->n <= 64 ? 64 : 128);
   if (M <= 64) {                     // a handful of rows (time-embedding MLP)
     pl.bm = M <= 32 ? 32 : 64;
