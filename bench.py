@@ -191,6 +191,8 @@ def main():
                          "sample: config 4's full clip sampling (encode -> 50 DDIM steps -> decode -> panoptic); "
                          "ae: config 1's VAE (autoencoder) training iteration")
     ap.add_argument("--clips", type=int, default=2, help="train mode: clips of T frames per GPU")
+    ap.add_argument("--zero", action="store_true",
+                    help="train mode: ZeRO-1 sharded AdamW (train_diffusion.sh:27 optimizer_zero_redundancy)")
     args = ap.parse_args()
     if args.mode == "train":
         return main_train(args)
@@ -433,7 +435,8 @@ def main_train(args):
                                beta_end=0.012, steps_offset=1, clip_sample=False, set_alpha_to_one=False,
                                weight="max_clamp_snr", max_snr=2.0, device=dev, verbose=False)
     step = LDMTrainStep(u, sched, lr=1e-4, weight_decay=0.05, clip_grad=1.0, self_condition=True,
-                        compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32, seed=1 + rank)
+                        compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32, seed=1 + rank,
+                        zero_redundancy=args.zero)
     B, L = args.clips * args.frames, args.latent
     g = torch.Generator().manual_seed(100 + rank)
     lat = (torch.randn(B, 4, L, L, generator=g)).to(dev)
@@ -464,7 +467,8 @@ def main_train(args):
             "config": {"workload": f"train iteration: self-cond fwd + fwd + bwd + clip + AdamW, {B} frames/GPU",
                        "model": "SD-1.4 UNet2DConditionModel, cross-attn removed, 12-ch conv_in (815.5M)",
                        "global_batch": B * world, "seq_len": L * L,
-                       "parallelism": f"dp{world} (RCCL bucketed all-reduce overlapped with backward)"},
+                       "parallelism": f"dp{world} (RCCL bucketed all-reduce overlapped with backward)"
+                                      + (", ZeRO-1 sharded AdamW" if args.zero and world > 1 else "")},
             "loss": round(lv, 6),
             "algorithmic_tflop_per_iter_per_gpu": round(tflop, 2),
             "achieved_tflops_per_gpu": round(tflop * args.steps / elapsed, 1),
