@@ -550,18 +550,32 @@ __global__ __launch_bounds__(256) void lnb_kernel(const T* __restrict__ x, const
       for (int o = G; o < 64; o <<= 1) { a += __shfl_xor(a, o, 64); b2 += __shfl_xor(b2, o, 64); }
       pg[i][k] = a; pb[i][k] = b2;
     }
-  if (lane < G) {
+  // then the block's 4 waves are summed in LDS (one wave after the other) and each channel
+  // gets ONE atomic per block: per-wave atomics put 4096 contended adds on every channel address
+  // (~1 ms per launch in the training profile, profiles/r02d_train_kernel_stats.csv)
+  constexpr int CMAX = G * NV * EPC;
+  __shared__ float red[2 * CMAX];
+  const int wave = threadIdx.x >> 6;
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w && lane < G) {
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int v = gl + G * i;
-      if (v < V) {
+      for (int i = 0; i < NV; ++i) {
+        const int v = gl + G * i;
+        if (v < V) {
 #pragma unroll
-        for (int k = 0; k < EPC; ++k) {
-          if (dgamma) atomicAdd(dgamma + v * EPC + k, pg[i][k]);
-          if (dbeta) atomicAdd(dbeta + v * EPC + k, pb[i][k]);
+          for (int k = 0; k < EPC; ++k) {
+            const int c = v * EPC + k;
+            red[c] = (w == 0 ? 0.f : red[c]) + pg[i][k];
+            red[CMAX + c] = (w == 0 ? 0.f : red[CMAX + c]) + pb[i][k];
+          }
         }
       }
     }
+    __syncthreads();
+  }
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    if (dgamma) atomicAdd(dgamma + c, red[c]);
+    if (dbeta) atomicAdd(dbeta + c, red[CMAX + c]);
   }
 }
 
@@ -752,7 +766,7 @@ int lnb_launch_g(const void* x, const void* dy, int rows, int c, const float* ga
   const int V = c / EPC;
   const int nv = (V + G - 1) / G;
   const int rpb = 4 * (64 / G);
-  const int grid = std::min((rows + rpb - 1) / rpb, 1024);
+  const int grid = std::min((rows + rpb - 1) / rpb, 512);
 #define LNB_CASE(NVC)                                                                                      \
   if (nv <= NVC) {                                                                                         \
     hipLaunchKernelGGL((lnb_kernel<T, G, NVC>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)dy, rows, c, \
