@@ -125,6 +125,11 @@ void ldm_conv2d_set_halo(int mode);
  * GEGLU, no time embedding / GroupNorm partials): 0 = planner's choice (the 64x64 UNet level),
  * 1 = never, 2 = whenever legal. */
 void ldm_conv2d_set_ars(int mode);
+/* Tuning hook: the wide-tile persistent bf16 1x1 GEMM (256 x 320 tiles, one 8-wave block per CU
+ * walking its tiles; N a multiple of 320, NHWC or GEGLU, no time embedding / split-K):
+ * 0 = planner's choice (>= 256 tiles), 1 = never, 2 = whenever legal (256-row tiles),
+ * 3 = whenever legal with 128-row tiles. */
+void ldm_conv2d_set_wide(int mode);
 /* Tuning hook: column width of the split-K reduction kernel's 64-row tiles — 0 = planner's choice
  * (64 when 128-wide tiles give fewer than 512 blocks), 64 or 128 forced. */
 void ldm_conv2d_set_splitk_cols(int cols);

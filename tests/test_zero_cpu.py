@@ -4,7 +4,9 @@ The reference wraps AdamW in ZeroRedundancyOptimizer when optimizer_zero_redunda
 (optim.py:71-78, tools/scripts/train_diffusion.sh:27) and consolidates the state before saving
 (trainers_ldm_cond.py:1844-1866).  Here: the two ranks' shards are disjoint and cover the flat
 buffer, every AdamW segment is split between them without loss, and a torch AdamW state loaded
-into the sharded optimizer comes back bit-identical from the (collective) state_dict().  The
+into the sharded optimizer comes back bit-identical from consolidate_state_dict() (collective) +
+state_dict() (local; it refuses an unconsolidated sharded state), through checkpoint.save called
+on every rank (rank 0 writes) and a resume on every rank.  The
 update arithmetic itself runs on the GPU (tests/test_gpu_train_full.py, ZeRO vs unsharded).
 """
 import os
@@ -23,7 +25,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, tmp):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -38,23 +40,46 @@ def _worker(rank, world, port, q):
         ts = LDMTrainStep(_unet(2 + rank), DDIMNoiseScheduler(), lr=1e-4, weight_decay=0.01, weight_decay_norm=0.0,
                           lr_factor_func=lr_func, zero_redundancy=True)
         ts.load_state_dict(ref.state_dict())
+        try:                                  # sharded state: state_dict() alone must refuse
+            ts.state_dict()
+            refused = False
+        except RuntimeError:
+            refused = True
+        ts.consolidate_state_dict()           # collective: every rank
         mine = ts.state_dict()
         theirs = ref.state_dict()
+        # checkpoint.save on every rank: consolidated collectively, written by rank 0 only
+        from ldmseg.utils import checkpoint
+        path = os.path.join(tmp, "model.pt")
+        checkpoint.save(path, unet=ts.unet, vae_semseg=torch.nn.Linear(1, 1), step=1, epoch=0, opt=ts)
+        dist.barrier()
+        saved = checkpoint.read(path)["opt"]
+        same_saved = all(torch.equal(saved["state"][i][k], theirs["state"][i][k])
+                         for i in theirs["state"] for k in ("exp_avg", "exp_avg_sq"))
+        # resume on every rank: a local load (no collective), same moments back
+        ts2 = LDMTrainStep(_unet(2), DDIMNoiseScheduler(), lr=1e-4, weight_decay=0.01, weight_decay_norm=0.0,
+                           lr_factor_func=lr_func, zero_redundancy=True)
+        ts2.load_state_dict(saved)
+        ts2.consolidate_state_dict()
+        back = ts2.state_dict()
+        same_resumed = all(torch.equal(back["state"][i][k], theirs["state"][i][k])
+                           for i in theirs["state"] for k in ("exp_avg", "exp_avg_sq"))
         same = mine["state"].keys() == theirs["state"].keys() and all(
             torch.equal(mine["state"][i][k], theirs["state"][i][k])
             for i in theirs["state"] for k in ("exp_avg", "exp_avg_sq"))
         q.put((rank, ts.shard, ts.exp_avg.numel(), ts.flat.numel, [list(s[:2]) for s in ts.seg_hp],
-               [s[:2] for s in ts.shard_segments()], same, ts.step_count, ts.flat.data.numpy().copy()))   # by value
+               [s[:2] for s in ts.shard_segments()], same and refused and same_saved and same_resumed, ts.step_count,
+               ts.flat.data.numpy().copy()))   # by value
     finally:
         dist.destroy_process_group()
 
 
-def test_zero1_shards_and_consolidated_state_world2():
+def test_zero1_shards_and_consolidated_state_world2(tmp_path):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, str(tmp_path))) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in range(world))

@@ -176,6 +176,8 @@ def main():
     ap.add_argument("--epi", type=int, default=0, help="conv epilogue mode (ldm_conv2d_set_epilogue)")
     ap.add_argument("--ars", nargs="*", type=int, default=[0],
                     help="short-K 1x1 GEMM modes to compare (ldm_conv2d_set_ars: 0 planner, 1 never, 2 when legal)")
+    ap.add_argument("--wide", nargs="*", type=int, default=[0],
+                    help="wide-tile persistent 1x1 GEMM modes (ldm_conv2d_set_wide: 0 planner, 1 never, 2 BM 256, 3 BM 128)")
     ap.add_argument("--skcols", nargs="*", type=int, default=[0],
                     help="split-K reduction tile widths to compare (ldm_conv2d_set_splitk_cols: 0 planner, 64, 128)")
     a = ap.parse_args()
@@ -190,22 +192,24 @@ def main():
             continue
         for pl in a.plans:
             for gm in a.groups:
-                for am, sk in [(x, y) for x in a.ars for y in a.skcols]:
+                for am, sk, wd in [(x, y, z) for x in a.ars for y in a.skcols for z in a.wide]:
                     run, fl, nb = CASES[n]()
                     f = [0, 0, 1, 0] if pl == "auto" else [int(v) for v in pl.split(",")] + [0]
                     bm, bn, ks, st = f[:4]
 
-                    def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm, am=am, sk=sk):
+                    def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm, am=am, sk=sk, wd=wd):
                         K.set_conv_splitk_cols(sk)
                         K.force_conv_plan(bm, bn, ks)
                         K.force_conv_stages(st)
                         K.set_conv_raster_group(gm)
                         K.set_conv_ars(am)
+                        K.set_conv_wide(wd)
                         return run()
                     name = n if pl == "auto" else f"{n}@{pl}"
                     name = name if len(a.groups) == 1 else f"{name}/g{gm}"
                     name = name if len(a.ars) == 1 else f"{name}/ars{am}"
-                    built[name if len(a.skcols) == 1 else f"{name}/skc{sk}"] = (run_pl, fl, nb)
+                    name = name if len(a.skcols) == 1 else f"{name}/skc{sk}"
+                    built[name if len(a.wide) == 1 else f"{name}/w{wd}"] = (run_pl, fl, nb)
     for n, (run, _, _) in built.items():
         run()
     torch.cuda.synchronize()

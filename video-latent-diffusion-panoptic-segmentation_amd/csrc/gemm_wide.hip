@@ -1,0 +1,351 @@
+// Wide-tile persistent 1x1 GEMM for the large-N transformer projections: the LayerNorm-folded
+// QKV (to_q/k/v of diffusers Attention) and GEGLU ff.net.0 of every BasicTransformerBlock that
+// the reference UNet runs through Transformer2DModel (/root/reference/ldmseg/models/unet.py:361-425).
+// Its own translation unit on the shared igemm helpers (igemm_common.h); ldm_conv2d (igemm.hip)
+// dispatches to it through ldm_igemm::wide_bm / launch_wide.
+//
+// Why: the 128x160 two-blocks-per-CU tiles receive 36 KB of operands per 64-deep K tile for
+// 2.6 MFLOP (71 FLOP/B) and their main loops are bound by operand delivery into LDS.
+// A 256x320 tile receives 72 KB per 64 of K for 10.5 MFLOP (146 FLOP/B).  Such a tile needs all of
+// a CU (8 waves of 64x160 fp32 accumulators, a 144 KB LDS ring), so the launch is persistent: one
+// block per CU walks its tiles (XCD-contiguous ids, grouped raster) and the LDS-DMA stream never
+// stops at a tile boundary.  Measured on the first (two-slot, 64-deep) form: with the MFMAs removed
+// the kernel ran exactly as long, with the loads removed 40 % shorter — the main loop waited on
+// the single K tile in flight (~28 GB/s per CU at 80 % L2 hits).  So the ring holds four 32-deep
+// K slices and keeps three in flight (108 KB) while one is multiplied.
+//
+// The epilogue runs from registers and never touches the ring: the next tile's first slices stream
+// in while it stores.  Per-tile column constants (bias, LayerNorm-fold column sums) and row
+// constants (LayerNorm-fold row statistics) arrive with the tile's first slice by LDS-DMA into a
+// small double-buffered scratch, so no compiler-visible global load is left in the kernel — such a
+// load would make hipcc wait vmcnt(0) and drain the prefetch.  Every wait on the DMA stream is a
+// counted vmcnt computed from the exact per-wave instruction counts (stores included: they are
+// issued as raw buffer stores, out-of-range rows dropped by the hardware range check, so their
+// count is fixed).
+//   NHWC (QKV): act(acc + bias) with the LayerNorm fold, packed to bf16; lanes (g, lr) and
+//     (g ^ 1, lr) exchange one fragment's halves so every lane stores 16 B (8 channels).
+//   GEGLU: h * gelu(g) from the hidden / gate fragment pair that shares a lane, 8-B stores.
+// Geometry: 512 threads = 8 waves as 4 (M) x 2 (N); wave tile 64 x 160 = 4 x 10 fragments of
+// v_mfma_f32_16x16x32_bf16 (D[n][m] = W . A^T: lane (g, lr) holds channels 4g..4g+3 of pixel lr).
+#include "igemm_common.h"
+
+namespace {
+namespace wide {
+constexpr int NT = 512;
+constexpr int BM = 256;
+constexpr int BN = 320;
+constexpr int WM = 64, WN = 160;    // wave tile: 4 waves along M, 2 along N
+constexpr int FM = WM / 16;         // 4 fragments along M
+constexpr int FN = WN / 16;         // 10 along N
+constexpr int KS = 32;              // K per ring slice (64 B per operand row)
+constexpr int NSLOT = 4;            // ring slots: three slices in flight while one is multiplied
+constexpr int SLOT_U4 = (BM + BN) * 4;      // uint4 per slot (36 KB)
+constexpr int A_INS = BM / 16 / 8;          // A DMA instructions per wave and slice (16 rows each)
+constexpr int B_INS_TOT = BN / 16;          // 20 B instructions per slice over 8 waves: 3 or 2
+// scratch floats per tile: bias [320] at 0, c1 [320] at 512, rows [256][2] at 1024 — six wave DMA
+// instructions of 256 floats, each from one source (the buffer descriptor is wave-uniform)
+constexpr int SCR_F = 1536;
+constexpr int SCR_C1 = 512, SCR_ROW = 1024;
+constexpr int NST = FM * FN / 2;            // epilogue store instructions per lane (20)
+// physical 16-B chunk of logical chunk c in 64-B row r: conflict-free ds_read_b128 for the
+// 16x16x32 fragment lanes (rows lr = 0..15, chunks g): h(r) = -(r >> 2) mod 4
+__device__ __forceinline__ int swz4(int r, int c) { return c ^ ((4 - ((r >> 2) & 3)) & 3); }
+}  // namespace wide
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate is an instruction field)
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+#define LDM_WV(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    LDM_WV(0) LDM_WV(1) LDM_WV(2) LDM_WV(3) LDM_WV(4) LDM_WV(5) LDM_WV(6) LDM_WV(7) LDM_WV(8) LDM_WV(9)
+    LDM_WV(10) LDM_WV(11) LDM_WV(12) LDM_WV(13) LDM_WV(14) LDM_WV(15) LDM_WV(16) LDM_WV(17) LDM_WV(18)
+    LDM_WV(19) LDM_WV(20) LDM_WV(21) LDM_WV(22) LDM_WV(23) LDM_WV(24) LDM_WV(25) LDM_WV(26) LDM_WV(27)
+    LDM_WV(28) LDM_WV(29) LDM_WV(30) LDM_WV(31) LDM_WV(32) LDM_WV(33) LDM_WV(34) LDM_WV(35) LDM_WV(36)
+    LDM_WV(37) LDM_WV(38) LDM_WV(39) LDM_WV(40) LDM_WV(41) LDM_WV(42) LDM_WV(43) LDM_WV(44) LDM_WV(45)
+    LDM_WV(46) LDM_WV(47) LDM_WV(48) LDM_WV(49) LDM_WV(50) LDM_WV(51) LDM_WV(52) LDM_WV(53) LDM_WV(54)
+    LDM_WV(55) LDM_WV(56) LDM_WV(57) LDM_WV(58) LDM_WV(59) LDM_WV(60) LDM_WV(61) LDM_WV(62)
+#undef LDM_WV
+    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
+  }
+}
+
+// GEGLU: the epilogue form (one instantiation per form)
+template <bool GEGLU>
+__global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
+  using namespace wide;
+  __shared__ uint4 smem[NSLOT * SLOT_U4 + 2 * SCR_F / 4];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 15, g = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  // DMA lane geometry: one wave instruction = 16 rows x 64 B; lane -> row lane >> 2, chunk lane & 3
+  const int drow = lane >> 2;
+  const int dchunk = (lane & 3) ^ ((4 - ((drow >> 2) & 3)) & 3);   // source-side swizzle
+  const int b_ins = (wv + 16 < B_INS_TOT) ? 3 : 2;                  // this wave's B instructions
+  const int scr_ins = wv < 6 ? 1 : 0;                               // scratch DMA (tile's first slice)
+
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int ntiles = tiles_m * p.tiles_n;
+  const int G = gridDim.x;
+  int vb;
+  {
+    const int bid = blockIdx.x, xcd = bid & 7, qq = G >> 3, rem = G & 7;
+    vb = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+  }
+  const int my_tiles = vb < ntiles ? (ntiles - 1 - vb) / G + 1 : 0;
+  const int nks = p.kpad / KS;
+  const int total = my_tiles * nks;
+
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+  const unsigned scr0 = lds0 + NSLOT * SLOT_U4 * 16;
+  float* scr = reinterpret_cast<float*>(smem + NSLOT * SLOT_U4);
+  const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)p.a0, 0, p.a0_bytes, kBufFlags);
+  const __amdgpu_buffer_rsrc_t ra1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(p.a1 ? p.a1 : p.a0), 0, p.a1 ? p.a1_bytes : 0, kBufFlags);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, p.w_bytes, kBufFlags);
+  const __amdgpu_buffer_rsrc_t rbias =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, 0, p.bias ? p.n * 4 : 0, kBufFlags);
+  const __amdgpu_buffer_rsrc_t rc1 =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_c1, 0, p.ln_rows ? p.n * 4 : 0, kBufFlags);
+  const __amdgpu_buffer_rsrc_t rrow =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_rows, 0, p.ln_rows ? p.M * 8 : 0, kBufFlags);
+  const int n_out = GEGLU ? (p.n >> 1) : p.n;
+  const __amdgpu_buffer_rsrc_t rout =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.out, 0, (int)((int64_t)p.M * n_out * 2), kBufFlags);
+
+  auto coords = [&](int r, int& m0, int& n0) {
+    int tm, tn;
+    grouped_tile(r * G + vb, tiles_m, p.tiles_n, p.group_m, tm, tn);
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  // DMA instructions this wave issues for slice s
+  auto per = [&](int s) { return A_INS + b_ins + ((s % nks) == 0 ? scr_ins : 0); };
+  // slice s of this block's stream = K slice (s mod nks) of its tile s / nks
+  auto issue = [&](int s) {
+    const int r = s / nks, kt = s - r * nks;
+    int m0, n0;
+    coords(r, m0, n0);
+    const unsigned abase = lds0 + (unsigned)((s & (NSLOT - 1)) * SLOT_U4 * 16);
+    const unsigned bbase = abase + BM * 64;
+    const int k0 = kt * KS;
+    const int sel = (p.c1 > 0 && k0 >= p.c0) ? 1 : 0;   // concat boundary is slice aligned (host)
+    const int cs = sel ? p.c1 : p.c0;
+    const int choff = (sel ? k0 - p.c0 : k0) + dchunk * 8;
+#pragma unroll
+    for (int i = 0; i < A_INS; ++i) {
+      const int q = wv + 8 * i;                         // instruction index: rows 16q .. 16q + 15
+      const int m = m0 + 16 * q + drow;
+      const int off = m < p.M ? (m * cs + choff) * 2 : kOOB;
+      const unsigned dst = __builtin_amdgcn_readfirstlane(abase + q * 16 * 64);
+      if (sel) dma16(ra1, off, dst);
+      else dma16(ra0, off, dst);
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int q = wv + 8 * i;
+      if (q < B_INS_TOT) {                              // wave-uniform
+        const int n = n0 + 16 * q + drow;
+        const int off = n < p.n ? (n * p.kpad + k0 + dchunk * 8) * 2 : kOOB;
+        dma16(rw, off, __builtin_amdgcn_readfirstlane(bbase + q * 16 * 64));
+      }
+    }
+    if (kt == 0 && scr_ins) {
+      // instruction wv: 0, 1 bias [256 wv, +256); 2, 3 c1; 4, 5 rows [m0 + 128 (wv - 4), +128)
+      const unsigned sb = scr0 + (unsigned)((r & 1) * SCR_F * 4) + wv * 1024;
+      const int e = (wv & 1) * 256 + lane * 4;          // first float of this lane's 16 B
+      int off;
+      if (wv < 4) off = e < BN ? (n0 + e) * 4 : kOOB;
+      else off = (m0 * 2 + e) * 4;
+      const unsigned dst = __builtin_amdgcn_readfirstlane(sb);
+      if (wv < 2) dma16(rbias, off, dst);
+      else if (wv < 4) dma16(rc1, off, dst);
+      else dma16(rrow, off, dst);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+  auto compute = [&](int slot) {
+    const uint4* As = smem + slot * SLOT_U4;
+    const uint4* Bs = As + BM * 4;
+    Frag8<bf16_t> af[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int r = wm * WM + i * 16 + lr;
+      af[i].v = As[r * 4 + swz4(r, g)];
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int r = wn * WN + j * 16 + lr;
+      Frag8<bf16_t> bf;
+      bf.v = Bs[r * 4 + swz4(r, g)];
+#ifdef LDM_ABL_NO_MFMA   // ablation build: fragments read from LDS, no MFMA issued
+      asm volatile("" ::"v"(bf.v.x), "v"(bf.v.w));
+      if (j == 0) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[i].v.x), "v"(af[i].v.w));
+      }
+      continue;
+#endif
+#pragma unroll
+      for (int i = 0; i < FM; ++i) mma_k32(acc[i][j], bf, af[i]);
+    }
+  };
+
+  int issued = 0;
+  for (; issued < total && issued < NSLOT - 1; ++issued) issue(issued);
+  int s = 0;
+  for (int r = 0; r < my_tiles; ++r) {
+    int m0, n0;
+    coords(r, m0, n0);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nks; ++kt, ++s) {
+      // slice s landed for this wave: the younger slices (and the previous tile's epilogue stores,
+      // issued after them) may stay in flight
+      int younger = 0;
+      for (int x = s + 1; x < issued; ++x) younger += per(x);
+      if (kt == 0 && r > 0) younger += NST;
+      wait_vm(younger);
+      // every wave's part of slice s is in LDS, and every wave is done with slot (s - 1) & 3
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      if (issued < total && issued <= s + NSLOT - 1) issue(issued++);
+      compute(s & (NSLOT - 1));
+    }
+    // ---- epilogue from registers; this tile's scratch landed with its first slice
+    const float* sbias = scr + (r & 1) * SCR_F;
+    const float* sc1 = sbias + SCR_C1;
+    const float2* srow = reinterpret_cast<const float2*>(sbias + SCR_ROW);
+    float2 lnr[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      if (p.ln_rows) {
+        const float2 st = srow[wm * WM + i * 16 + lr];
+        const float mean = st.x * p.ln_inv_k;
+        const float rstd = rsqrtf(fmaxf(st.y * p.ln_inv_k - mean * mean, 0.f) + p.ln_eps);
+        lnr[i] = make_float2(rstd, -rstd * mean);
+      } else {
+        lnr[i] = make_float2(1.f, 0.f);
+      }
+    }
+    if constexpr (GEGLU) {
+#pragma unroll
+      for (int j = 0; j < FN; j += 2) {
+        const int cl = wn * WN + j * 16 + 4 * g;                 // tile column of the hidden values
+        const int oc = ((n0 + cl) >> 5) * 16 + ((n0 + cl) & 15); // output channel
+        const float4 bh = *reinterpret_cast<const float4*>(sbias + cl);
+        const float4 bg = *reinterpret_cast<const float4*>(sbias + cl + 16);
+        const float4 ch = *reinterpret_cast<const float4*>(sc1 + cl);
+        const float4 cg = *reinterpret_cast<const float4*>(sc1 + cl + 16);
+        const float bhv[4] = {bh.x, bh.y, bh.z, bh.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+        const float chv[4] = {ch.x, ch.y, ch.z, ch.w}, cgv[4] = {cg.x, cg.y, cg.z, cg.w};
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int m = m0 + wm * WM + i * 16 + lr;
+          const float2 rs = lnr[i];
+          bf16_t h[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            h[k] = f2bf(fmaf(rs.y, chv[k], fmaf(rs.x, acc[i][j][k], bhv[k])) *
+                        gelu_f(fmaf(rs.y, cgv[k], fmaf(rs.x, acc[i][j + 1][k], bgv[k]))));
+          const uint2 u = *reinterpret_cast<const uint2*>(h);
+          const int off = (m < p.M && n0 + cl < p.n) ? (int)(((int64_t)m * n_out + oc) * 2) : kOOB;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, u),
+                                                rout, off, 0, 0);
+        }
+      }
+    } else {
+      // act(acc + bias), LayerNorm fold; lanes g and g ^ 1 trade halves of a fragment pair so each
+      // stores 8 consecutive channels: even g -> fragment j channels 4g..4g+7, odd g -> fragment
+      // j + 1 channels 4(g-1)..4(g-1)+7 (16 + ... of the pair)
+      const bool odd = g & 1;
+#pragma unroll
+      for (int j = 0; j < FN; j += 2) {
+        const int c0 = wn * WN + j * 16 + 4 * g;                 // this lane's columns in fragment j
+        const float4 b0 = *reinterpret_cast<const float4*>(sbias + c0);
+        const float4 b1 = *reinterpret_cast<const float4*>(sbias + c0 + 16);
+        const float4 k0 = *reinterpret_cast<const float4*>(sc1 + c0);
+        const float4 k1 = *reinterpret_cast<const float4*>(sc1 + c0 + 16);
+        const float bv0[4] = {b0.x, b0.y, b0.z, b0.w}, bv1[4] = {b1.x, b1.y, b1.z, b1.w};
+        const float kv0[4] = {k0.x, k0.y, k0.z, k0.w}, kv1[4] = {k1.x, k1.y, k1.z, k1.w};
+        // the stored 8 columns: even g: c0 .. c0 + 7 of fragment j; odd g: c0 + 12 .. c0 + 19
+        const int cst = odd ? c0 + 12 : c0;
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int m = m0 + wm * WM + i * 16 + lr;
+          const float2 rs = lnr[i];
+          float v0[4], v1[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v0[k] = act_f(fmaf(rs.y, kv0[k], fmaf(rs.x, acc[i][j][k], bv0[k])), p.act);
+            v1[k] = act_f(fmaf(rs.y, kv1[k], fmaf(rs.x, acc[i][j + 1][k], bv1[k])), p.act);
+          }
+          bf16_t h0[4] = {f2bf(v0[0]), f2bf(v0[1]), f2bf(v0[2]), f2bf(v0[3])};
+          bf16_t h1[4] = {f2bf(v1[0]), f2bf(v1[1]), f2bf(v1[2]), f2bf(v1[3])};
+          const uint2 u0 = *reinterpret_cast<const uint2*>(h0), u1 = *reinterpret_cast<const uint2*>(h1);
+          // send the half the partner stores: even sends fragment j + 1, odd sends fragment j
+          const uint2 snd = odd ? u0 : u1;
+          uint2 rcv;
+          rcv.x = __shfl_xor((int)snd.x, 16, 64);
+          rcv.y = __shfl_xor((int)snd.y, 16, 64);
+          const uint4 out = odd ? make_uint4(rcv.x, rcv.y, u1.x, u1.y) : make_uint4(u0.x, u0.y, rcv.x, rcv.y);
+          const int off = (m < p.M && n0 + cst < p.n) ? (int)(((int64_t)m * p.n + n0 + cst) * 2) : kOOB;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, out),
+                                                 rout, off, 0, 0);
+        }
+      }
+    }
+  }
+}
+}  // namespace
+
+namespace ldm_igemm {
+
+// legal: bf16 1x1 GEMM (one source, or a concat whose boundary is 32-channel aligned), N a
+// multiple of 320, NHWC (bias / activation / LayerNorm fold) or GEGLU (bias / LayerNorm fold); no
+// residual, row or GroupNorm statistics, time embedding, split-K or fp32 output
+static int g_wide_mode = 0;   // tuning hook: 0 planner, 1 never, 2 whenever legal
+bool wide_legal(const ldm_conv_params* q, int es, bool mixed) {
+  const auto a16 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; };
+  if (es != 2 || mixed || q->ksize != 1 || q->stride != 1 || q->upsample || q->pad_mode != 0) return false;
+  // >= 4 K slices per tile: a tile's scratch buffer is rewritten only after its epilogue
+  if (q->c0 % wide::KS || q->c1 % wide::KS || q->kpad % wide::KS || q->kpad < 4 * wide::KS || q->n % wide::BN)
+    return false;
+  if (q->out_layout != LDM_OUT_NHWC && q->out_layout != LDM_OUT_GEGLU) return false;
+  if (q->out_f32 || q->temb || q->residual || q->row_stats || q->gn_partial) return false;
+  if (q->out_layout == LDM_OUT_GEGLU && q->act != LDM_ACT_NONE) return false;
+  if (!a16(q->out) || !a16(q->bias) || !a16(q->ln_c1)) return false;
+  if (q->ln_rows && (reinterpret_cast<uintptr_t>(q->ln_rows) & 15)) return false;
+  const int64_t M = (int64_t)q->batch * q->h_out * q->w_out;
+  if (M * q->n * 2 >= (1LL << 31) - 64 || M * 8 >= (1LL << 31)) return false;
+  return true;
+}
+
+// rows per tile for this call, 0 = not the wide kernel
+int wide_bm(const ldm_conv_params* q, int es, bool mixed, int M, bool plan_forced) {
+  if (g_wide_mode == 1 || plan_forced || !wide_legal(q, es, mixed)) return 0;
+  if (g_wide_mode == 2) return wide::BM;
+  const int tiles = ((M + wide::BM - 1) / wide::BM) * (q->n / wide::BN);
+  // enough tiles to give every CU one, K deep enough to amortise the per-tile epilogue
+  if (tiles >= 256 && q->kpad >= 320) return wide::BM;
+  return 0;
+}
+
+int launch_wide(ConvArgs a, hipStream_t s, int bm) {
+  if (bm != wide::BM) return LDM_ERR_ARG;
+  a.tiles_n = a.n / wide::BN;
+  const int ntiles = ((a.M + wide::BM - 1) / wide::BM) * a.tiles_n;
+  const int grid = std::min(ntiles, 256);
+  a.nblk = grid;
+  if (a.out_layout == LDM_OUT_GEGLU) hipLaunchKernelGGL((gemm_wide_kernel<true>), dim3(grid), dim3(wide::NT), 0, s, a);
+  else hipLaunchKernelGGL((gemm_wide_kernel<false>), dim3(grid), dim3(wide::NT), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+}  // namespace ldm_igemm
+
+extern "C" void ldm_conv2d_set_wide(int mode) { ldm_igemm::g_wide_mode = (mode >= 1 && mode <= 2) ? mode : 0; }

@@ -22,705 +22,14 @@
 // chunk — the GroupNorm statistics of the tensor it just wrote, so the following GroupNorm
 // never re-reads it for statistics.
 // bf16: v_mfma_f32_16x16x32_bf16; fp32: v_mfma_f32_16x16x4_f32 (exact) — same code.
-#include "common.h"
+#include "igemm_common.h"
+
+namespace ldm_igemm {   // gemm_wide.hip
+int wide_bm(const ldm_conv_params* q, int es, bool mixed, int M, bool plan_forced);
+int launch_wide(ConvArgs a, hipStream_t s, int bm);
+}  // namespace ldm_igemm
 
 namespace {
-
-struct ConvArgs {
-  const char* a0;
-  const char* a1;
-  int a0_bytes, a1_bytes;
-  int c0, c1, cin;
-  int h_in, w_in, h_out, w_out, hw_out;
-  int ksize, stride, upsample, pad;
-  const char* w;
-  int w_bytes;
-  int n, kpad, K;
-  const float* bias;
-  const float* temb;
-  int temb_stride;
-  const char* residual;
-  char* out;
-  int out_layout, act, out_f32;
-  int M;
-  int tiles_n, nblk;
-  int mixed_src;      // the concat boundary is not K-tile aligned: per-lane source select
-  int ksplit;         // > 1: write fp32 partials to `partial` [ksplit][M][n]
-  float* partial;
-  double* gn_part;    // optional [batch][gn_slots][n / gn_unit][2] fp64 (sum, sumsq) accumulators of
-                      // the stored output (zeroed by the caller; each tile adds one fp32 partial
-                      // per gn_unit-channel unit atomically, into slot (tile row index) % gn_slots)
-  int gn_unit, gn_slots;
-  int epi_pre;        // 1: the bf16 pre-activated staging epilogue where legal (A/B hook)
-  float* row_stats;   // optional [M][2] (sum, sumsq) of every stored output row (atomic adds)
-  const float* ln_rows;   // optional LayerNorm fold: [M][2] (sum, sumsq) of the A rows ...
-  const float* ln_c1;     // ... and [n] column sums of the gamma-scaled weight
-  float ln_inv_k, ln_eps;
-  int tap_inner;      // K tiles visited channel-block-major, taps inner (see k_state)
-  int group_m;        // M panels per raster group (grouped_tile); 1 = plain row-major tiles
-};
-
-constexpr int kBufFlags = 0x00020000;
-constexpr int kOOB = 0x7ffffff0;  // offset past every num_records: the load returns zeros
-
-__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
-
-
-// Grouped raster: tile ids run over groups of 8 M panels with the N tiles outer inside a
-// group, so the ~64 tiles an XCD has in flight at once (its contiguous run of ids, see the
-// kernels) share 8 A panels and a few B column tiles from that XCD's L2 instead of streaming
-// all of B once per M panel (GEGLU 640: L2 misses 283 -> ~60 MB per launch).
-__device__ __forceinline__ void grouped_tile(int tile, int tiles_m, int tiles_n, int G, int& tm, int& tn) {
-  const int span = G * tiles_n;
-  const int grp = tile / span, idx = tile - grp * span;
-  const int rows = min(G, tiles_m - grp * G);
-  tm = grp * G + idx % rows;
-  tn = idx / rows;
-}
-
-// Order in which a block visits its K tiles.  Packed K is tap-major (ky, kx, c), but when
-// every tile lies inside one tap (cin % BK == 0) the tiles are visited channel-block-major
-// with the 9 taps innermost: the same 64 input channels of the same input rows are then
-// re-read 9 times within 9 consecutive tiles (an L2 hit) instead of once per tap sweep
-// (which, at the 64x64 level, falls out of the XCD's 4 MB L2 into the Infinity Cache).
-// Per lane: ch = channel of its 16-B chunk, (tap, ky, kx), kofs = packed-K offset.
-struct KState {
-  int ch, tap, ky, kx, kofs;
-  __device__ __forceinline__ void init(const ConvArgs& p, int kt0, int bk, int lane_k) {
-    const int ntaps = p.ksize * p.ksize;
-    if (p.tap_inner) {
-      const int cb = kt0 / ntaps;
-      tap = kt0 - cb * ntaps;
-      ch = cb * bk + lane_k;
-      kofs = tap * p.cin + ch;
-    } else {
-      ch = kt0 * bk + lane_k;
-      kofs = ch;
-      tap = ch / p.cin;
-      ch -= tap * p.cin;
-    }
-    ky = tap / p.ksize;
-    kx = tap - ky * p.ksize;
-  }
-  __device__ __forceinline__ bool valid(const ConvArgs& p) const { return tap < p.ksize * p.ksize && ch < p.cin; }
-  __device__ __forceinline__ void advance(const ConvArgs& p, int bk) {
-    if (p.tap_inner) {
-      ++tap;
-      if (++kx == p.ksize) { kx = 0; ++ky; }
-      if (tap == p.ksize * p.ksize) { tap = 0; ky = 0; kx = 0; ch += bk; }
-      kofs = tap * p.cin + ch;
-    } else {
-      kofs += bk;
-      ch += bk;
-      while (ch >= p.cin) {
-        ch -= p.cin;
-        ++tap;
-        if (++kx == p.ksize) { kx = 0; ++ky; }
-      }
-    }
-  }
-};
-
-__device__ __forceinline__ uint4 bload(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-
-// 16 B per lane global -> LDS (LDS address = M0 + 16 * lane).  Inline asm on purpose: hipcc
-// would otherwise drain every in-flight LDS-DMA (vmcnt(0)) before the next ds_read of ANY LDS
-// buffer, serialising the prefetch of tile k+1 with the MFMAs of tile k.  The caller owns the
-// wait: `s_waitcnt vmcnt(0)` + barrier before the buffer is read.  M0 is saved and restored.
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, int voff, unsigned lds_addr) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(lds_addr)
-      : "memory");
-}
-
-template <typename T>
-__device__ __forceinline__ void store4(char* base, int64_t idx, const float* v, bool f32out) {
-  if (f32out || sizeof(T) == 4) {
-    *reinterpret_cast<float4*>(base + idx * 4) = make_float4(v[0], v[1], v[2], v[3]);
-  } else {
-    bf16_t h[4] = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
-    *reinterpret_cast<uint2*>(base + idx * 2) = *reinterpret_cast<const uint2*>(h);
-  }
-}
-template <typename T>
-__device__ __forceinline__ void store1(char* base, int64_t idx, float v, bool f32out) {
-  if (f32out || sizeof(T) == 4) reinterpret_cast<float*>(base)[idx] = v;
-  else reinterpret_cast<bf16_t*>(base)[idx] = f2bf(v);
-}
-template <typename T>
-__device__ __forceinline__ void load4(const char* base, int64_t idx, float* v) {
-  if constexpr (sizeof(T) == 2) {
-    const uint2 rv = *reinterpret_cast<const uint2*>(base + idx * 2);
-    const bf16_t* h = reinterpret_cast<const bf16_t*>(&rv);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = bf2f(h[r]);
-  } else {
-    const float4 rv = *reinterpret_cast<const float4*>(base + idx * 4);
-    v[0] = rv.x; v[1] = rv.y; v[2] = rv.z; v[3] = rv.w;
-  }
-}
-
-// Finish 4 consecutive output channels [n, n+4) of row m from raw accumulators: + bias,
-// + time embedding (both preloaded by the caller: they depend only on the column / batch),
-// activation, + residual (NHWC: preloaded into `res`), store.  `v` returns the stored values.
-template <typename T>
-__device__ __forceinline__ void finish4(const ConvArgs& p, int b, int pix, int m, int n, float* v,
-                                        const float* bias4, const float* temb4, const float* res) {
-  const int N = p.n;
-  const bool f32o = p.out_f32 != 0;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    v[r] = act_f(v[r] + bias4[r] + temb4[r], p.act);
-  }
-  if (p.out_layout == LDM_OUT_NCHW) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (n + r >= N) break;
-      const int64_t idx = ((int64_t)b * N + n + r) * p.hw_out + pix;
-      if (p.residual) v[r] += to_f(reinterpret_cast<const T*>(p.residual)[idx]);
-      store1<T>(p.out, idx, v[r], f32o);
-    }
-    return;
-  }
-  int64_t idx;
-  if (p.out_layout == LDM_OUT_NHWC) {
-    idx = (int64_t)m * N + n;
-    if (p.residual) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] += res[r];
-    }
-  } else {  // LDM_OUT_SHUFFLE2: n = (dy*2+dx)*Cout + co -> output pixel (2y+dy, 2x+dx)
-    const int cout = N >> 2;
-    const int qd = n / cout, co = n - qd * cout;
-    const int y = pix / p.w_out, x = pix - y * p.w_out;
-    idx = (((int64_t)b * 2 * p.h_out + 2 * y + (qd >> 1)) * 2 * p.w_out + 2 * x + (qd & 1)) * cout + co;
-    if (p.residual) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (n + r < N) v[r] += to_f(reinterpret_cast<const T*>(p.residual)[idx + r]);
-    }
-  }
-  if (n + 3 < N) {
-    store4<T>(p.out, idx, v, f32o);
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (n + r >= N) { v[r] = 0.f; continue; }
-      store1<T>(p.out, idx + r, v[r], f32o);
-    }
-  }
-}
-
-// Floats of the epilogue's GroupNorm scratch `red`: one record of HALVES x CPC (sum, sumsq)
-// pairs per thread, padded by 4 (CPC 8: ds_write_b128) or 2 (CPC 4: ds_write_b64) floats so
-// consecutive threads' records start in different banks (unpadded, a 64-float record put all 16
-// lanes of a b128 write in one bank group: a 16-way conflict).
-template <int NT, int COLS, int ROWS, int CPC>
-constexpr int gn_red_stride() { return (ROWS >= 64 ? ROWS / 64 : 1) * CPC * 2 + (CPC == 8 ? 4 : 2); }
-template <int NT, int COLS, int ROWS, int CPC>
-constexpr int gn_red_floats() { return (NT / (COLS / CPC)) * (COLS / CPC) * gn_red_stride<NT, COLS, ROWS, CPC>(); }
-
-// GroupNorm statistics: a run of 64-row chunks' fp32 (sum, sumsq) of one gn_unit-channel unit
-// into the batch's fp64 accumulators, slot `slot` of gn_slots (the GroupNorm consumer sums the
-// slots and finalises per-group mean / rstd).  Same-address atomics serialise at the memory-side
-// atomic unit, so the slots spread the tiles of one batch over gn_slots copies.
-__device__ __forceinline__ void gn_accumulate(const ConvArgs& p, int batch, int slot, int unit, float a, float b) {
-  double* acc = p.gn_part + (((int64_t)batch * p.gn_slots + slot) * (p.n / p.gn_unit) + unit) * 2;
-  unsafeAtomicAdd(acc, (double)a);
-  unsafeAtomicAdd(acc + 1, (double)b);
-}
-
-// Final step of the epilogue's GroupNorm statistics.  On entry thread `tid` holds the (sum,
-// sumsq) over the tile rows of one 64-row chunk half for the elements e = tid + i * NT,
-// e = (c * HALVES + hh) * CPC + k <-> tile column CPC * c + k.  They are parked in `red` (all
-// earlier reads of it are complete), then every gn_unit-channel unit of the tile is summed over
-// its columns and over the halves of one batch, and added to its accumulator: one atomic pair
-// per (unit, batch) of the tile, not per (channel, 64-row chunk) (a unit split by a tile edge
-// gets one partial from each tile).
-template <int HALVES, int CPC, int COLS, int NT, int EPT>
-__device__ __forceinline__ void gn_units_out(const ConvArgs& p, int m0, int n0, int tid, const float* ra,
-                                             const float* rb, float* red) {
-  constexpr int NE = (COLS / CPC) * HALVES * CPC;
-#ifdef LDM_ABL_GN_NO_UNITS   // ablation build: per-channel reduction kept, unit sums / atomics dropped
-  if (ra[0] == 12345.f) red[tid] = rb[0];
-  return;
-#endif
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < EPT; ++i) {
-    const int e = tid + i * NT;
-    if (e < NE) { red[2 * e] = ra[i]; red[2 * e + 1] = rb[i]; }
-  }
-  __syncthreads();
-  const int U = p.gn_unit;
-  const int nend = min(n0 + COLS, p.n);
-  const int ufirst = n0 / U, nu = (nend - 1) / U - ufirst + 1;
-  const int c0 = m0 >> 6;                                  // first chunk of this epilogue
-  const int slot = (c0 / HALVES) % p.gn_slots;
-  for (int t = tid; t < nu; t += NT) {
-    const int uu = ufirst + t;
-    const int cb = max(uu * U, n0) - n0, ce = min((uu + 1) * U, nend) - n0;
-    float a = 0.f, b = 0.f;
-    int bat = (c0 * 64) / p.hw_out;
-    for (int hh = 0; hh < HALVES; ++hh) {
-      const int chunk = c0 + hh;
-      if (chunk * 64 >= p.M) break;
-      const int cb_bat = (chunk * 64) / p.hw_out;
-      if (cb_bat != bat) {                                 // the tile crosses into the next batch
-        gn_accumulate(p, bat, slot, uu, a, b);
-        a = b = 0.f;
-        bat = cb_bat;
-      }
-      for (int col = cb; col < ce; ++col) {
-        const int e = ((col / CPC) * HALVES + hh) * CPC + col % CPC;
-        a += red[2 * e];
-        b += red[2 * e + 1];
-      }
-    }
-    gn_accumulate(p, bat, slot, uu, a, b);
-  }
-}
-
-// Phase 2 of the epilogue, shared by the fused path (raw values staged in LDS) and the
-// split-K reduction (raw values summed from the fp32 slab).  `raw(r, c4, v)` fills 4 raw
-// values of local row r, local 4-channel chunk c4.  Rows [0, ROWS), channels [0, COLS),
-// NT threads.  Threads sweep (row, chunk) with chunk fastest -> coalesced row segments; a
-// thread's columns are fixed, so bias (and the time embedding per batch) are loaded once,
-// and rows go in groups of GP whose raw values and residuals are all fetched before any is
-// finished — the global loads of a group overlap instead of forming a latency chain.
-// With gn_part set, per-channel (sum, sumsq) over each 64-row chunk of the stored values
-// is reduced through `red` ([RP][CW][ROWS/64][4][2] floats) and added to the chunk's batch
-// accumulators in gn_part (fp64 atomics; a chunk never spans two batches: hw % 64 == 0).
-template <typename T, int ROWS, int COLS, int NT, typename RawFn>
-__device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0, RawFn raw, float* red) {
-  constexpr int CW = COLS / 4;           // chunks per row
-  constexpr int RP = NT / CW;            // rows per pass
-  constexpr int NP = (ROWS + RP - 1) / RP;
-  constexpr int GP = 4;                  // rows in flight per thread
-  constexpr int HALVES = ROWS / 64 > 0 ? ROWS / 64 : 1;
-  constexpr int RS = gn_red_stride<NT, COLS, ROWS, 4>();
-  const int tid = threadIdx.x;
-  const int c4 = tid % CW, r0 = tid / CW;
-  const int N = p.n;
-  const bool stats = p.gn_part != nullptr;
-  if (p.out_layout == LDM_OUT_GEGLU) {
-    constexpr int OCW = CW / 2;          // GEGLU output chunks per row (half width)
-    constexpr int ORP = NT / OCW;
-    constexpr int ONP = (ROWS + ORP - 1) / ORP;
-    const int oc4 = tid % OCW, or0 = tid / OCW;
-    const int oc = (n0 >> 1) + 4 * oc4;
-    if (or0 >= ORP || oc >= (N >> 1)) return;
-    const int lc = 4 * oc4;                       // local output column
-    const int pcl = (lc >> 4) * 32 + (lc & 15);   // local packed column of the hidden half
-    const int pc = (oc >> 4) * 32 + (oc & 15);    // global packed column
-    float bh[4], bg[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      bh[k] = p.bias ? p.bias[pc + k] : 0.f;
-      bg[k] = p.bias ? p.bias[pc + 16 + k] : 0.f;
-    }
-#pragma unroll
-    for (int q0 = 0; q0 < ONP; q0 += GP) {
-      float h[GP][4], gt[GP][4];
-#pragma unroll
-      for (int q = 0; q < GP; ++q) {
-        const int r = or0 + (q0 + q) * ORP;
-        if (q0 + q < ONP && r < ROWS) {
-          raw(r, pcl >> 2, h[q]);
-          raw(r, (pcl + 16) >> 2, gt[q]);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < GP; ++q) {
-        const int r = or0 + (q0 + q) * ORP;
-        if (q0 + q >= ONP || r >= ROWS || m0 + r >= p.M) continue;
-        float v[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = (h[q][k] + bh[k]) * gelu_f(gt[q][k] + bg[k]);
-        store4<T>(p.out, (int64_t)(m0 + r) * (N >> 1) + oc, v, p.out_f32 != 0);
-      }
-    }
-    return;
-  }
-  float s[HALVES][4], sq[HALVES][4];
-#pragma unroll
-  for (int hh = 0; hh < HALVES; ++hh)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { s[hh][k] = 0.f; sq[hh][k] = 0.f; }
-  const int n = n0 + 4 * c4;
-  if (r0 < RP && n < N) {
-    float bias4[4], temb4[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) bias4[k] = p.bias ? p.bias[min(n + k, N - 1)] : 0.f;
-    int tb = -1;                                   // batch whose temb4 is loaded
-    const bool nhwc_res = p.residual && p.out_layout == LDM_OUT_NHWC;
-    // (batch, pixel) of this thread's first row, then advanced by RP rows without divisions
-    int bb = (m0 + r0) / p.hw_out;
-    int pix = (m0 + r0) - bb * p.hw_out;
-#pragma unroll
-    for (int q0 = 0; q0 < NP; q0 += GP) {
-      float v[GP][4], rv[GP][4];
-      int bq[GP], pq[GP];
-#pragma unroll
-      for (int q = 0; q < GP; ++q) {
-        const int r = r0 + (q0 + q) * RP;
-        bq[q] = bb; pq[q] = pix;
-        pix += RP;
-        while (pix >= p.hw_out) { pix -= p.hw_out; ++bb; }
-        if (q0 + q >= NP || r >= ROWS || m0 + r >= p.M) continue;
-        raw(r, c4, v[q]);
-        if (nhwc_res) {
-          const int64_t idx = (int64_t)(m0 + r) * N + n;
-          if (n + 3 < N) {
-            load4<T>(p.residual, idx, rv[q]);
-          } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-              rv[q][k] = n + k < N ? to_f(reinterpret_cast<const T*>(p.residual)[idx + k]) : 0.f;
-          }
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < GP; ++q) {
-        const int r = r0 + (q0 + q) * RP;
-        if (q0 + q >= NP || r >= ROWS || m0 + r >= p.M) continue;
-        if (p.temb && bq[q] != tb) {
-          tb = bq[q];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) temb4[k] = p.temb[(int64_t)tb * p.temb_stride + min(n + k, N - 1)];
-        }
-        finish4<T>(p, bq[q], pq[q], m0 + r, n, v[q], bias4, temb4, rv[q]);
-        if (stats) {
-          const int hh = HALVES > 1 ? (r >> 6) : 0;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            // statistics of the value as stored (bf16-rounded on the bf16 path)
-            const float x = (sizeof(T) == 2 && !p.out_f32) ? bf2f(f2bf(v[q][k])) : v[q][k];
-            s[hh][k] += x;
-            sq[hh][k] += x * x;
-          }
-        }
-      }
-    }
-  }
-  if (!stats) return;
-#ifdef LDM_ABL_GN_ROWS_ONLY  // ablation build: row sums kept, no block reduction / atomics
-  if (s[0][0] == 12345.f) red[tid] = sq[0][0];
-  return;
-#endif
-  __syncthreads();
-  if (r0 < RP) {
-#pragma unroll
-    for (int hh = 0; hh < HALVES; ++hh)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        red[(r0 * CW + c4) * RS + (hh * 4 + k) * 2 + 0] = s[hh][k];
-        red[(r0 * CW + c4) * RS + (hh * 4 + k) * 2 + 1] = sq[hh][k];
-      }
-  }
-  __syncthreads();
-  constexpr int EPT = (CW * HALVES * 4 + NT - 1) / NT;
-  float ra[EPT], rb[EPT];
-#pragma unroll
-  for (int i = 0; i < EPT; ++i) {
-    const int e = tid + i * NT;
-    const int k = e & 3, hh = (e >> 2) % HALVES, c = e / (4 * HALVES);
-    float a = 0.f, b = 0.f;
-    if (e < CW * HALVES * 4 && n0 + 4 * c + k < N)
-      for (int rg = 0; rg < RP; ++rg) {
-        a += red[(rg * CW + c) * RS + (hh * 4 + k) * 2 + 0];
-        b += red[(rg * CW + c) * RS + (hh * 4 + k) * 2 + 1];
-      }
-    ra[i] = a;
-    rb[i] = b;
-  }
-  gn_units_out<HALVES, 4, COLS, NT, EPT>(p, m0, n0, tid, ra, rb, red);
-}
-
-// Fast epilogue for the common bf16 cases (NHWC with bias / time embedding / SiLU / residual /
-// GroupNorm partials, and GEGLU): each thread owns 8 consecutive channels (one 16-B store per
-// row), all of a thread's residual and time-embedding loads are issued before any value is
-// finished, and nothing in the row loop branches on the layout.  `stage` is the fp32 tile
-// [ROWS][pitch] in LDS; `red` may alias it (it is written only after a barrier).
-// Returns false (nothing done) when the call needs the generic epilogue_rows.
-__device__ __forceinline__ bool fast_epilogue_ok(const ConvArgs& p) {
-  const auto a16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
-  return !p.out_f32 && (p.out_layout == LDM_OUT_NHWC || p.out_layout == LDM_OUT_GEGLU) && (p.n & 7) == 0 &&
-         a16(p.out) && a16(p.residual) && a16(p.bias) && a16(p.temb) && (p.temb_stride & 3) == 0;
-}
-__device__ __forceinline__ void unpack8(const uint4 u, float* v) {
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    v[2 * k] = __uint_as_float(w[k] << 16);
-    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
-  }
-}
-__device__ __forceinline__ uint4 pack8(const float* v) {
-  bf16_t h[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) h[k] = f2bf(v[k]);
-  return *reinterpret_cast<const uint4*>(h);
-}
-
-// LayerNorm fold: (rstd, -rstd * mean) of A row m from its (sum, sumsq)
-__device__ __forceinline__ float2 ln_row(const ConvArgs& p, int m) {
-  const float2 st = *reinterpret_cast<const float2*>(p.ln_rows + 2 * (int64_t)m);
-  const float mean = st.x * p.ln_inv_k;
-  const float var = fmaxf(st.y * p.ln_inv_k - mean * mean, 0.f);
-  const float rstd = rsqrtf(var + p.ln_eps);
-  return make_float2(rstd, -rstd * mean);
-}
-
-// rows [m0, m0 + rows) cover at most two batches (the fast path holds two time embeddings)
-__device__ __forceinline__ bool fast_temb_ok(const ConvArgs& p, int m0, int rows) {
-  return !p.temb || (min(m0 + rows, p.M) - 1) / p.hw_out - m0 / p.hw_out <= 1;
-}
-
-// PRE: the staged tile already holds the final pre-residual values as bf16 (bias, time
-// embedding and activation applied from the accumulators by the caller, `pitch` in bf16
-// elements); only the residual, the stores and the GroupNorm statistics are left.
-template <int ROWS, int COLS, int NT, bool PRE = false>
-__device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0, const void* stage_v, int pitch,
-                                              float* red) {
-  const int tid = threadIdx.x;
-  const int N = p.n;
-  const float* stage = reinterpret_cast<const float*>(stage_v);
-  if (!PRE && p.out_layout == LDM_OUT_GEGLU) {
-    constexpr int OCW = COLS / 16;             // 8-wide output chunks per row
-    constexpr int ORP = NT / OCW;
-    constexpr int ONP = (ROWS + ORP - 1) / ORP;
-    const int oc8 = tid % OCW, r0 = tid / OCW;
-    const int lc = 8 * oc8;
-    const int oc = (n0 >> 1) + lc;
-    if (r0 >= ORP || oc >= (N >> 1)) return;
-    const int pcl = (lc >> 4) * 32 + (lc & 15);
-    const int pc = (oc >> 4) * 32 + (oc & 15);
-    float bh[8], bg[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      bh[k] = p.bias ? p.bias[pc + k] : 0.f;
-      bg[k] = p.bias ? p.bias[pc + 16 + k] : 0.f;
-    }
-    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
-#pragma unroll
-    for (int q = 0; q < ONP; ++q) {
-      const int r = r0 + q * ORP;
-      if (r >= ROWS || m0 + r >= p.M) break;
-      const float* srow = stage + r * pitch;
-      float v[8];
-#pragma unroll
-      for (int k = 0; k < 8; k += 4) {
-        const float4 h = *reinterpret_cast<const float4*>(srow + pcl + k);
-        const float4 g = *reinterpret_cast<const float4*>(srow + pcl + 16 + k);
-        v[k] = (h.x + bh[k]) * gelu_f(g.x + bg[k]);
-        v[k + 1] = (h.y + bh[k + 1]) * gelu_f(g.y + bg[k + 1]);
-        v[k + 2] = (h.z + bh[k + 2]) * gelu_f(g.z + bg[k + 2]);
-        v[k + 3] = (h.w + bh[k + 3]) * gelu_f(g.w + bg[k + 3]);
-      }
-      *reinterpret_cast<uint4*>(out + (int64_t)(m0 + r) * (N >> 1) + oc) = pack8(v);
-    }
-    return;
-  }
-  constexpr int CW = COLS / 8;                 // 16-B chunks per row
-  constexpr int RP = NT / CW;                  // rows per pass
-  constexpr int NP = (ROWS + RP - 1) / RP;
-  constexpr int HALVES = ROWS >= 64 ? ROWS / 64 : 1;
-  constexpr int RS = gn_red_stride<NT, COLS, ROWS, 8>();
-  const int c8 = tid % CW, r0 = tid / CW;
-  const int n = n0 + 8 * c8;
-  const bool act = r0 < RP && n < N;
-  const bool stats = p.gn_part != nullptr;
-  float s[HALVES][8], sq[HALVES][8];
-#pragma unroll
-  for (int hh = 0; hh < HALVES; ++hh)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { s[hh][k] = 0.f; sq[hh][k] = 0.f; }
-  float rsum[NP], rsq[NP];                       // PRE + row_stats: this thread's part of each row
-#pragma unroll
-  for (int q = 0; q < NP; ++q) { rsum[q] = 0.f; rsq[q] = 0.f; }
-  if (act) {
-    float add[8];
-#pragma unroll
-    for (int k = 0; k < 8; k += 4) {
-      const float4 b4 = (!PRE && p.bias) ? *reinterpret_cast<const float4*>(p.bias + n + k)
-                                         : make_float4(0.f, 0.f, 0.f, 0.f);
-      add[k] = b4.x; add[k + 1] = b4.y; add[k + 2] = b4.z; add[k + 3] = b4.w;
-    }
-    const bf16_t* res = reinterpret_cast<const bf16_t*>(p.residual);
-    bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
-    // the tile's rows span at most two batches (fast_temb_ok): their time embeddings
-    const int b0 = m0 / p.hw_out;
-    const int bsplit = (b0 + 1) * p.hw_out;          // first row of batch b0 + 1
-    float4 te0[2], te1[2];
-    if (!PRE && p.temb) {
-      const float* tp = p.temb + (int64_t)b0 * p.temb_stride + n;
-      te0[0] = *reinterpret_cast<const float4*>(tp);
-      te0[1] = *reinterpret_cast<const float4*>(tp + 4);
-      if (bsplit < min(m0 + ROWS, p.M)) {
-        te1[0] = *reinterpret_cast<const float4*>(tp + p.temb_stride);
-        te1[1] = *reinterpret_cast<const float4*>(tp + p.temb_stride + 4);
-      } else {
-        te1[0] = te0[0];
-        te1[1] = te0[1];
-      }
-    }
-    constexpr int GP = NP < 3 ? NP : 3;             // rows whose residual loads are in flight together
-#pragma unroll
-    for (int q0 = 0; q0 < NP; q0 += GP) {
-      uint4 rv[GP];
-#pragma unroll
-      for (int q = 0; q < GP; ++q) {
-        const int r = r0 + (q0 + q) * RP;
-        if (res && q0 + q < NP && r < ROWS && m0 + r < p.M)
-          rv[q] = *reinterpret_cast<const uint4*>(res + (int64_t)(m0 + r) * N + n);
-      }
-#pragma unroll
-      for (int q = 0; q < GP; ++q) {
-        const int r = r0 + (q0 + q) * RP;
-        const int m = m0 + r;
-        if (q0 + q >= NP || r >= ROWS || m >= p.M) break;
-        float v[8];
-        if constexpr (PRE) {
-          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(stage_v) + r * pitch + 8 * c8), v);
-        } else {
-          const float* srow = stage + r * pitch + 8 * c8;
-          const float4 x0 = *reinterpret_cast<const float4*>(srow);
-          const float4 x1 = *reinterpret_cast<const float4*>(srow + 4);
-          v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] += add[k];
-          if (p.temb) {
-            const bool second = m >= bsplit;
-            const float4 ta = second ? te1[0] : te0[0], tb = second ? te1[1] : te0[1];
-            v[0] += ta.x; v[1] += ta.y; v[2] += ta.z; v[3] += ta.w;
-            v[4] += tb.x; v[5] += tb.y; v[6] += tb.z; v[7] += tb.w;
-          }
-          if (p.act != LDM_ACT_NONE) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) v[k] = act_f(v[k], p.act);
-          }
-        }
-        if (res) {
-          float rr[8];
-          unpack8(rv[q], rr);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] += rr[k];
-        }
-        const uint4 packed = pack8(v);
-#ifdef LDM_ABL_EPI_NO_STORE   // ablation build: the epilogue's math kept, its global stores dropped
-        if (packed.x == 0x12345678u && packed.y == 0x9abcdef0u) *reinterpret_cast<uint4*>(out + (int64_t)m * N + n) = packed;
-#else
-        *reinterpret_cast<uint4*>(out + (int64_t)m * N + n) = packed;
-#endif
-        if (stats) {
-          float st[8];
-          unpack8(packed, st);                   // statistics of the value as stored
-          const int hh = HALVES > 1 ? (r >> 6) : 0;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { s[hh][k] += st[k]; sq[hh][k] += st[k] * st[k]; }
-        }
-        if (PRE && p.row_stats) {
-          float st[8];
-          unpack8(packed, st);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { rsum[q0 + q] += st[k]; rsq[q0 + q] += st[k] * st[k]; }
-        }
-      }
-    }
-  }
-  if (PRE && p.row_stats) {
-    // reduce each row's CW partials through LDS (rows x CW (sum, sumsq), after every stage read),
-    // then one atomic pair per (row, tile)
-    __syncthreads();
-    if (r0 < RP) {
-#pragma unroll
-      for (int q = 0; q < NP; ++q) {
-        const int r = r0 + q * RP;
-        if (r < ROWS) {
-          red[(r * CW + c8) * 2] = rsum[q];
-          red[(r * CW + c8) * 2 + 1] = rsq[q];
-        }
-      }
-    }
-    __syncthreads();
-    for (int r = tid; r < ROWS; r += NT) {
-      if (m0 + r >= p.M) break;
-      float a = 0.f, b = 0.f;
-      for (int c = 0; c < CW && n0 + 8 * c < N; ++c) {
-        a += red[(r * CW + c) * 2];
-        b += red[(r * CW + c) * 2 + 1];
-      }
-      atomicAdd(p.row_stats + 2 * (int64_t)(m0 + r), a);
-      atomicAdd(p.row_stats + 2 * (int64_t)(m0 + r) + 1, b);
-    }
-  }
-  if (!stats) return;
-#ifdef LDM_ABL_GN_ROWS_ONLY  // ablation build: row sums kept, no block reduction / atomics
-  if (s[0][0] == 12345.f) red[tid] = sq[0][0];
-  return;
-#endif
-  __syncthreads();                             // every stage read is done: red may alias it
-  if (r0 < RP) {
-#pragma unroll
-    for (int hh = 0; hh < HALVES; ++hh)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        red[(r0 * CW + c8) * RS + hh * 16 + 2 * k] = s[hh][k];
-        red[(r0 * CW + c8) * RS + hh * 16 + 2 * k + 1] = sq[hh][k];
-      }
-  }
-  __syncthreads();
-  constexpr int EPT = (CW * HALVES * 8 + NT - 1) / NT;
-  float ra[EPT], rb[EPT];
-#pragma unroll
-  for (int i = 0; i < EPT; ++i) {
-    const int e = tid + i * NT;
-    const int k = e & 7, hh = (e >> 3) % HALVES, c = e / (8 * HALVES);
-    float a = 0.f, b = 0.f;
-    if (e < CW * HALVES * 8 && n0 + 8 * c + k < N)
-      for (int rg = 0; rg < RP; ++rg) {
-        a += red[(rg * CW + c) * RS + hh * 16 + 2 * k];
-        b += red[(rg * CW + c) * RS + hh * 16 + 2 * k + 1];
-      }
-    ra[i] = a;
-    rb[i] = b;
-  }
-  gn_units_out<HALVES, 8, COLS, NT, EPT>(p, m0, n0, tid, ra, rb, red);
-}
-
-// Split-K: raw fp32 accumulators of a staged [ROWS][pitch] tile -> this split's slab
-// [M][N] as full coalesced rows (16 B per lane; a 160-column row is 640 contiguous bytes).
-template <int ROWS, int COLS, int NT>
-__device__ __forceinline__ void write_partial_rows(const ConvArgs& p, float* part, int m0, int n0,
-                                                   const float* stage, int pitch) {
-  constexpr int CW = COLS / 4, RP = NT / CW, NP = (ROWS + RP - 1) / RP;
-  const int tid = threadIdx.x, c4 = tid % CW, r0 = tid / CW;
-  const int n = n0 + 4 * c4;
-  if (r0 >= RP || n >= p.n) return;
-#pragma unroll
-  for (int q = 0; q < NP; ++q) {
-    const int r = r0 + q * RP, m = m0 + r;
-    if (r >= ROWS || m >= p.M) break;
-    const float4 x = *reinterpret_cast<const float4*>(stage + r * pitch + 4 * c4);
-    float* dst = part + (int64_t)m * p.n + n;
-    if (n + 3 < p.n) {
-      *reinterpret_cast<float4*>(dst) = x;
-    } else {
-      const float v[4] = {x.x, x.y, x.z, x.w};
-      for (int k = 0; k < 4 && n + k < p.n; ++k) dst[k] = v[k];
-    }
-  }
-}
 
 template <typename T, int BM, int BN, bool DMA, int NS = 2>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
@@ -1978,7 +1287,7 @@ extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   if (validate(q, &es) != LDM_OK) return 0;
   const int M = q->batch * q->h_out * q->w_out;
   const bool mixed = is_mixed(q, es);
-  if (use_halo_plan(q, es, mixed) || use_ars(q, es, mixed, M)) return 0;
+  if (use_halo_plan(q, es, mixed) || ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0) || use_ars(q, es, mixed, M)) return 0;
   const Plan pl = make_plan(q, M, es, mixed);
   return pl.ksplit > 1 ? (size_t)pl.ksplit * M * q->n * sizeof(float) : 0;
 }
@@ -1992,8 +1301,9 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   const int M = q->batch * q->h_out * q->w_out;
   const bool mixed = is_mixed(q, es);
   const bool use_halo = use_halo_plan(q, es, mixed);
-  const bool ars = !use_halo && use_ars(q, es, mixed, M);
-  const Plan pl = (use_halo || ars) ? Plan{0, 0, 1} : make_plan(q, M, es, mixed);
+  const int wbm = use_halo ? 0 : ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0);
+  const bool ars = !use_halo && !wbm && use_ars(q, es, mixed, M);
+  const Plan pl = (use_halo || wbm || ars) ? Plan{0, 0, 1} : make_plan(q, M, es, mixed);
   if (pl.ksplit > 1) {
     const size_t need = (size_t)pl.ksplit * M * q->n * sizeof(float);
     if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;
@@ -2034,6 +1344,7 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.ln_eps = q->ln_eps;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (use_halo) return launch_halo(a, s);
+  if (wbm) return ldm_igemm::launch_wide(a, s, wbm);
   if (ars) return launch_ars(a, s);
   if (pl.bm == 256) return launch_big(a, s);
   const int stages = g_force_stages ? g_force_stages : pl.stages;

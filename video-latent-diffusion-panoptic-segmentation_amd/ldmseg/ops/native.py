@@ -66,6 +66,7 @@ EXPORTS = {
     "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_conv2d_set_halo": (None, [_i]),
     "ldm_conv2d_set_ars": (None, [_i]),
+    "ldm_conv2d_set_wide": (None, [_i]),
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
@@ -534,6 +535,12 @@ def set_conv_halo(mode=0):
 def set_conv_ars(mode=0):
     """Tuning hook: A-register-stationary short-K 1x1 GEMM — 0 planner, 1 never, 2 whenever legal."""
     load_library().ldm_conv2d_set_ars(int(mode))
+
+
+def set_conv_wide(mode=0):
+    """Tuning hook: wide-tile persistent 1x1 GEMM — 0 planner, 1 never, 2 whenever legal (256-row
+    tiles), 3 whenever legal (128-row tiles)."""
+    load_library().ldm_conv2d_set_wide(int(mode))
 
 
 def set_conv_splitk_cols(cols=0):

@@ -20,9 +20,13 @@ import torch.distributed as dist
 
 class FlatParams:
     """Re-home ``params`` (in the given order) into one flat fp32 data buffer and one flat fp32
-    grad buffer; every parameter's ``.data`` and ``.grad`` become views into them."""
+    grad buffer; every parameter's ``.data`` and ``.grad`` become views into them.
 
-    def __init__(self, params, device=None):
+    ``pad_to`` (>= the parameters' total) sizes the data storage: ``self.storage`` holds
+    ``pad_to`` elements (the tail zero) and ``self.data`` is its first ``numel``, so a ZeRO-1
+    all-gather of equal shards can write straight into it."""
+
+    def __init__(self, params, device=None, pad_to=None):
         params = list(params)
         if not params:
             raise ValueError("no trainable parameters")
@@ -34,7 +38,8 @@ class FlatParams:
             self.offsets.append(n)
             n += p.numel()
         self.numel = n
-        self.data = torch.empty(n, dtype=torch.float32, device=device)
+        self.storage = torch.zeros(max(n, pad_to or 0), dtype=torch.float32, device=device)
+        self.data = self.storage[:n]
         self.grad = torch.zeros(n, dtype=torch.float32, device=device)
         for p, o in zip(params, self.offsets):
             k = p.numel()

@@ -94,7 +94,12 @@ class LDMTrainStep:
         norm_ids = {id(q) for m in unet.modules() if isinstance(m, NORM_TYPES) for q in m.parameters(recurse=False)}
         order = unet_backward_order(unet)
         dev = order[0].device
-        self.flat = FlatParams(order, dev)
+        # ZeRO-1 shards are S elements (a multiple of 64) so the all-gather moves equal pieces;
+        # the flat storage is padded to S x world once, so the gather writes straight into it
+        self.zero = bool(zero_redundancy) and self.world > 1
+        n = sum(p.numel() for p in order)
+        self.shard_len = -(-n // (64 * self.world)) * 64 if self.zero else n
+        self.flat = FlatParams(order, dev, pad_to=self.shard_len * self.world if self.zero else None)
         self.bucketer = GradBucketer(self.flat, bucket_mb * 2 ** 20, group)
         lr_factor_func = lr_factor_func or unet.get_lr_func
         self.base_lr = lr
@@ -108,13 +113,10 @@ class LDMTrainStep:
             wd = weight_decay_norm if id(p) in norm_ids else weight_decay
             self.seg_hp.append([o, o + p.numel(), plr, wd])
             self.seg_key.append((plr, wd if id(p) in norm_ids else None))
-        # ZeRO-1 shard [lo, hi) of the flat buffer (the whole buffer without it); shards are
-        # S elements (a multiple of 64) so the all-gather moves equal pieces
-        self.zero = bool(zero_redundancy) and self.world > 1
-        n = self.flat.numel
+        # ZeRO-1 shard [lo, hi) of the flat buffer (the whole buffer without it)
+        self._consolidated = None
         if self.zero:
             self.rank = dist.get_rank(group)
-            self.shard_len = -(-n // (64 * self.world)) * 64
             lo = min(self.rank * self.shard_len, n)
             self.shard = (lo, min(lo + self.shard_len, n))
         else:
@@ -171,9 +173,16 @@ class LDMTrainStep:
         return buf[:self.flat.numel]
 
     def _gather_parameters(self):
-        """ZeroRedundancyOptimizer.step's parameter sync: every rank's updated shard to all."""
-        lo, hi = self.shard
-        self.flat.data.copy_(self._full(self.flat.data[lo:hi]))
+        """ZeroRedundancyOptimizer.step's parameter sync: every rank's updated shard to all.  On
+        RCCL an in-place all-gather into the padded flat storage (this rank's shard is already in
+        place: no temporary); gloo (no CUDA all-gather) sums zero-padded copies."""
+        S, r = self.shard_len, self.rank
+        st = self.flat.storage
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_gather_into_tensor(st, st[r * S:(r + 1) * S], group=self.group)
+        else:
+            lo, hi = self.shard
+            self.flat.data.copy_(self._full(self.flat.data[lo:hi]))
 
     def set_lr(self, lr):
         """update_scheduler (trainers_ldm_cond.py:783-790): the scheduled lr replaces EVERY
@@ -204,11 +213,26 @@ class LDMTrainStep:
         d.pop("params")
         return d
 
+    def consolidate_state_dict(self):
+        """ZeroRedundancyOptimizer.consolidate_state_dict: COLLECTIVE under ZeRO (every rank of
+        the group must call it); gathers the sharded AdamW moments so that state_dict() can then
+        be called on any rank alone (e.g. rank 0 inside checkpoint.save).  No-op without ZeRO."""
+        if self.zero:
+            self._consolidated = (self.step_count, self._full(self.exp_avg), self._full(self.exp_avg_sq))
+
     def state_dict(self):
-        """torch.optim.AdamW.state_dict() of the same optimizer (fp32 moments, ``step``).  Under
-        ZeRO this is collective (ZeroRedundancyOptimizer.consolidate_state_dict): every rank
-        returns the whole state."""
-        exp_avg, exp_avg_sq = self._full(self.exp_avg), self._full(self.exp_avg_sq)
+        """torch.optim.AdamW.state_dict() of the same optimizer (fp32 moments, ``step``).  Local
+        (never a collective).  Under ZeRO it needs consolidate_state_dict() on every rank first,
+        as torch's ZeroRedundancyOptimizer does, and raises otherwise — a rank-0-only save can
+        then never block inside a collective the other ranks do not join."""
+        if self.zero:
+            c = self._consolidated
+            if c is None or c[0] != self.step_count:
+                raise RuntimeError("ZeRO optimizer state is sharded: call consolidate_state_dict() on every "
+                                   "rank (checkpoint.save does) before state_dict()")
+            exp_avg, exp_avg_sq = c[1], c[2]
+        else:
+            exp_avg, exp_avg_sq = self.exp_avg, self.exp_avg_sq
         state, pgs, idx = {}, [], 0
         for _, ps in self.reference_param_groups():
             _, _, lr, wd = self.seg_hp[self.flat.index[id(ps[0])]]        # the group's current lr
@@ -223,9 +247,13 @@ class LDMTrainStep:
             pgs.append({**self._group_defaults(lr, wd), "params": ids})
         return {"state": state, "param_groups": pgs}
 
-    def load_state_dict(self, sd):
+    def load_state_dict(self, sd, broadcast=False):
         """Inverse of state_dict(); also accepts a reference run's AdamW state_dict when its
-        parameter grouping matches (same lr factors / weight decays)."""
+        parameter grouping matches (same lr factors / weight decays).  Local by default: every
+        rank loads the same checkpoint, as the reference's resume does on all ranks
+        (trainers_ldm_cond.py:1879-1914).  ``broadcast=True`` is COLLECTIVE (every rank must
+        call it): rank 0's moments, step count and learning rates replace the other ranks' —
+        for a state loaded on rank 0 only."""
         groups = self.reference_param_groups()
         exp_avg = torch.zeros_like(self.flat.data)          # whole-buffer moments, sharded below
         exp_avg_sq = torch.zeros_like(self.flat.data)
@@ -249,9 +277,7 @@ class LDMTrainStep:
         if len(steps) > 1:
             raise ValueError("per-parameter step counts differ; the fused AdamW keeps one count")
         self.step_count = steps.pop() if steps else 0
-        if self.world > 1:
-            # collective: every rank resumes (trainers_ldm_cond.py:1879-1914 runs on all ranks);
-            # rank 0's moments, step count and learning rates win, like its parameters at init
+        if broadcast and self.world > 1:
             dev = self.flat.data.device
             cnt = torch.tensor([float(self.step_count)], dtype=torch.float64, device=dev)
             hp = torch.tensor([[s[2], s[3]] for s in self.seg_hp], dtype=torch.float32, device=dev)

@@ -56,8 +56,13 @@ def construct_save_dict(unet, vae_semseg, vae_image=None, step=0, epoch=None, em
 
 
 def save(path, **kw):
-    """rank-0 ``torch.save(construct_save_dict(...), path)`` (:1869-1877)."""
+    """rank-0 ``torch.save(construct_save_dict(...), path)`` (:1869-1877).  Call it on EVERY
+    rank: a sharded (ZeRO) optimizer is consolidated collectively first, then rank 0 alone
+    builds and writes the dict."""
     import torch.distributed as dist
+    opt = kw.get("opt")
+    if hasattr(opt, "consolidate_state_dict"):
+        opt.consolidate_state_dict()
     if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
         return
     torch.save(construct_save_dict(**kw), str(path))
