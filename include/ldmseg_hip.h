@@ -386,9 +386,12 @@ int ldm_conv2d_wgrad(const ldm_wgrad_params* p, ldm_stream_t stream);
 
 /* ldm_colsum — out[s][c] (+)= sum over the rows of segment s of x[rows][c] (segments split the
  * rows evenly).  Bias gradients (1 segment) and per-batch time-embedding gradients (batch
- * segments).  geglu: columns are the packed GEGLU interleave, out is un-interleaved. fp32 out. */
-int ldm_colsum(const void* x, int rows, int c, int segments, int geglu, float* out, int accumulate, int dtype,
-               ldm_stream_t stream);
+ * segments).  geglu: columns are the packed GEGLU interleave, out is un-interleaved. fp32 out.
+ * Deterministic: 256-row chunks write an fp32 slab (workspace, ldm_colsum_workspace_bytes)
+ * that a second pass sums in chunk order — no atomics, bit-identical run to run. */
+size_t ldm_colsum_workspace_bytes(int rows, int c, int segments);
+int ldm_colsum(const void* x, int rows, int c, int segments, int geglu, float* out, int accumulate,
+               void* workspace, int dtype, ldm_stream_t stream);
 
 /* ldm_group_norm_bwd — backward of ldm_group_norm_ex (act NONE or SILU) given the saved
  * (mean, rstd).  dx of the two sources goes to dx0 [rows][c0] / dx1 [rows][c1]; acc0/acc1 add
@@ -402,10 +405,12 @@ int ldm_group_norm_bwd(const void* x0, const void* x1, int c0, int c1, int batch
                        ldm_stream_t stream);
 
 /* ldm_layer_norm_bwd — LayerNorm backward over [rows][c]; dx = LN'(dy) + add_src (the residual
- * stream's gradient).  dgamma/dbeta fp32 [c]. */
+ * stream's gradient).  dgamma/dbeta fp32 [c] (acc_params: +=).  Deterministic: per-block partials
+ * to a slab (workspace, ldm_layer_norm_bwd_workspace_bytes) summed in block order. */
+size_t ldm_layer_norm_bwd_workspace_bytes(int rows, int c);
 int ldm_layer_norm_bwd(const void* x, const void* dy, int rows, int c, const float* gamma, float eps,
-                       const void* add_src, void* dx, float* dgamma, float* dbeta, int acc_params, int dtype,
-                       ldm_stream_t stream);
+                       const void* add_src, void* dx, float* dgamma, float* dbeta, int acc_params,
+                       void* workspace, int dtype, ldm_stream_t stream);
 
 /* ldm_geglu — diffusers GEGLU on the packed GEMM output hg [rows][2f] ([h16 | g16] blocks):
  * dout == NULL: out[rows][f] = h * gelu(g);  else dhg[rows][2f] = (dout gelu(g), dout h gelu'(g)). */
@@ -423,10 +428,14 @@ int ldm_sum_pool2(const void* x, int batch, int h_out, int w_out, int c, void* o
  * target fp32 NCHW, mask fp32 [batch][hw] or NULL, weights fp32 [num_weights] or NULL. */
 int ldm_mse_loss(const void* pred, const float* target, const float* mask, const int64_t* t,
                  const float* weights, int num_weights, int batch, int ch, int hw, float grad_scale,
-                 void* dpred, double* loss_sum, int dtype, ldm_stream_t stream);
+                 void* dpred, double* loss_sum, void* workspace, int dtype, ldm_stream_t stream);
 
 /* ldm_sq_norm — *sum (+)= sum g^2 over a flat fp32 buffer (fp64 accumulation, device). */
-int ldm_sq_norm(const float* g, int64_t n, double* sum, int accumulate, ldm_stream_t stream);
+int ldm_sq_norm(const float* g, int64_t n, double* sum, int accumulate, void* workspace, ldm_stream_t stream);
+
+/* Workspace of ldm_mse_loss / ldm_sq_norm: per-block fp64 partials, summed in a fixed order by a
+ * second one-block pass (deterministic; no atomics). */
+size_t ldm_reduce_workspace_bytes(void);
 
 /* ldm_adamw — torch.optim.AdamW step over flat fp32 buffers (param, grad, exp_avg, exp_avg_sq).
  * segments: device array of {int64 begin, int64 end, float lr, float weight_decay} (24 B each,

@@ -45,6 +45,20 @@ def test_ops_refuse_cpu_tensors():
         K.bit_encode(torch.zeros(4, 4, dtype=torch.int64), 5, 255, 0.5)
 
 
+def test_group_norm_refuses_out_of_range_shapes_before_launch():
+    """ldm_group_norm stages <= 64 groups and <= 2560 channels in LDS; wider calls get a clear
+    error on the host (no launch, no GPU needed)."""
+    x = torch.zeros(1, 4, 128)
+    g, b = torch.ones(128), torch.zeros(128)
+    with pytest.raises(ValueError, match="outside the HIP kernel's range"):
+        K.group_norm(x, 1, 4, 128, g, b, 1e-5)            # 128 groups
+    x = torch.zeros(1, 4, 2600)
+    with pytest.raises(ValueError, match="outside the HIP kernel's range"):
+        K.group_norm(x, 1, 4, 26, torch.ones(2600), torch.zeros(2600), 1e-5)
+    with pytest.raises(RuntimeError, match="GPU tensors only"):   # in range: reaches the device check
+        K.group_norm(torch.zeros(1, 4, 2560), 1, 4, 32, torch.ones(2560), torch.zeros(2560), 1e-5)
+
+
 # --------------------------------------------------------------------------- UNet structure
 def test_unet_structure_and_param_counts():
     u = UNet()

@@ -232,9 +232,11 @@ __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ pa
 // ======================================================================================
 // column sums: out[seg][c] (+)= sum_{rows of seg} x[row][c]
 // ======================================================================================
+// Deterministic: every (row chunk, segment) block writes its column sums to its own row of the
+// fp32 slab part[chunk][segment][C] (no atomics); slab_reduce then sums the chunks in order.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, int C, int rows_per_seg, int rchunk,
-                                                     int geglu, float* __restrict__ out) {
+                                                     int geglu, float* __restrict__ part) {
   constexpr int EPC = 16 / sizeof(T);
   const int V = C / EPC;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -266,9 +268,42 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, in
         const int blk = c >> 5, w = c & 31, half = C >> 1;
         c = (w < 16) ? blk * 16 + w : half + blk * 16 + (w - 16);
       }
-      atomicAdd(out + (int64_t)seg * C + c, t);
+      part[((int64_t)blockIdx.y * gridDim.z + seg) * C + c] = t;
     }
   }
+}
+
+// out[i] (+)= sum_{q < nparts} part[q * stride + i], i < width, in the fixed order q = 0, 1, ...
+// (the deterministic second pass of the slab reductions: column sums, LayerNorm dgamma / dbeta)
+__global__ __launch_bounds__(256) void slab_reduce(const float* __restrict__ part, int nparts, int64_t stride,
+                                                   int64_t width, float* __restrict__ out, int accumulate) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= width) return;
+  float s = 0.f;
+  int q = 0;
+  for (; q + 4 <= nparts; q += 4) {          // four loads in flight, summed in order
+    const float a = part[(int64_t)q * stride + i], b = part[(int64_t)(q + 1) * stride + i];
+    const float c = part[(int64_t)(q + 2) * stride + i], d = part[(int64_t)(q + 3) * stride + i];
+    s += a; s += b; s += c; s += d;
+  }
+  for (; q < nparts; ++q) s += part[(int64_t)q * stride + i];
+  out[i] = accumulate ? out[i] + s : s;
+}
+
+// *sum (+)= sum_{q < n} part[q] (fp64), one block, fixed-order tree: the deterministic second pass of
+// the loss and gradient-norm reductions
+__global__ __launch_bounds__(256) void dsum_final(const double* __restrict__ part, int n, double* __restrict__ sum,
+                                                  int accumulate) {
+  __shared__ double red[256];
+  double a = 0.0;
+  for (int q = threadIdx.x; q < n; q += 256) a += part[q];
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *sum = accumulate ? *sum + red[0] : red[0];
 }
 
 // ======================================================================================
@@ -467,13 +502,13 @@ __global__ __launch_bounds__(256) void gnb_apply(const T* __restrict__ x0, const
 // ======================================================================================
 // LayerNorm backward: one wave-group of G lanes per row (as the forward), stats recomputed.
 //   dx = rstd (g - mean(g) - x_hat mean(g x_hat)),  g = gamma dy;  + add_src
-//   dgamma += dy x_hat, dbeta += dy  (block partials, fp32 atomics)
+//   dgamma += dy x_hat, dbeta += dy  (block partials to a slab, summed in order by slab_reduce)
 // ======================================================================================
 template <typename T, int G, int NV>
 __global__ __launch_bounds__(256) void lnb_kernel(const T* __restrict__ x, const T* __restrict__ dy, int rows, int C,
                                                   const float* __restrict__ gamma, float eps,
                                                   const T* __restrict__ add_src, T* __restrict__ dx,
-                                                  float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                  float* __restrict__ part) {
   constexpr int EPC = 16 / sizeof(T);
   constexpr int RPW = 64 / G;
   const int lane = threadIdx.x & 63;
@@ -571,9 +606,10 @@ __global__ __launch_bounds__(256) void lnb_kernel(const T* __restrict__ x, const
       for (int o = G; o < 64; o <<= 1) { a += __shfl_xor(a, o, 64); b2 += __shfl_xor(b2, o, 64); }
       pg[i][k] = a; pb[i][k] = b2;
     }
-  // then the block's 4 waves are summed in LDS (one wave after the other) and each channel
-  // gets ONE atomic per block: per-wave atomics put 4096 contended adds on every channel address
-  // (~1 ms per launch in the training profile, profiles/r02d_train_kernel_stats.csv)
+  // then the block's 4 waves are summed in LDS (one wave after the other, fixed order) and the
+  // block writes its row of the [grid][2][C] slab (per-wave atomics had put 4096 contended adds on
+  // every channel address, ~1 ms per launch, profiles/r02d_train_kernel_stats.csv; one atomic per
+  // block left the sum order to the hardware)
   constexpr int CMAX = G * NV * EPC;
   __shared__ float red[2 * CMAX];
   const int wave = threadIdx.x >> 6;
@@ -594,9 +630,10 @@ __global__ __launch_bounds__(256) void lnb_kernel(const T* __restrict__ x, const
     }
     __syncthreads();
   }
+  float* row = part + (int64_t)blockIdx.x * 2 * C;
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    if (dgamma) atomicAdd(dgamma + c, red[c]);
-    if (dbeta) atomicAdd(dbeta + c, red[CMAX + c]);
+    row[c] = red[c];
+    row[C + c] = red[CMAX + c];
   }
 }
 
@@ -688,7 +725,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void mse_kernel(const T* __restrict__ pred, const float* __restrict__ target,
                                                   const float* __restrict__ mask, const int64_t* __restrict__ t,
                                                   const float* __restrict__ wtab, int ntab, int batch, int ch, int hw,
-                                                  float grad_scale, T* __restrict__ dpred, double* __restrict__ sum) {
+                                                  float grad_scale, T* __restrict__ dpred, double* __restrict__ part) {
   const int64_t total = (int64_t)batch * ch * hw;
   double acc = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
@@ -708,13 +745,13 @@ __global__ __launch_bounds__(256) void mse_kernel(const T* __restrict__ pred, co
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(sum, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 // ======================================================================================
 // optimizer: sum of squares (fp64 accumulation) and fused AdamW over flat fp32 buffers
 // ======================================================================================
-__global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ sum) {
+__global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g, int64_t n, double* __restrict__ part) {
   double acc = 0.0;
   const int64_t n4 = n / 4;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
@@ -727,7 +764,7 @@ __global__ __launch_bounds__(256) void sqnorm_kernel(const float* __restrict__ g
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(sum, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
 }
 
 struct AdamSeg {
@@ -775,24 +812,36 @@ __global__ __launch_bounds__(256) void adamw_kernel(float* __restrict__ p, const
   }
 }
 
+constexpr int DSUM_MAX_PARTS = 2048;   // per-block fp64 partials of the loss / norm reductions
+
 int grid_for(int64_t work, int per_block, int cap) {
   const int64_t b = (work + per_block - 1) / per_block;
   return (int)std::max<int64_t>(1, std::min<int64_t>(b, cap));
 }
 
+constexpr int LNB_MAX_GRID = 512;
+int lnb_params(const float* part, int grid, int c, float* dg, float* db, int acc, hipStream_t s) {
+  if (hipGetLastError() != hipSuccess) return LDM_ERR_LAUNCH;
+  const dim3 rg((c + 255) / 256);
+  if (dg) hipLaunchKernelGGL(slab_reduce, rg, dim3(256), 0, s, part, grid, (int64_t)2 * c, (int64_t)c, dg, acc);
+  if (db) hipLaunchKernelGGL(slab_reduce, rg, dim3(256), 0, s, part + c, grid, (int64_t)2 * c, (int64_t)c, db, acc);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
 template <typename T, int G>
 int lnb_launch_g(const void* x, const void* dy, int rows, int c, const float* gamma, float eps, const void* add,
-                 void* dx, float* dg, float* db, hipStream_t s) {
+                 void* dx, float* dg, float* db, int acc, float* part, hipStream_t s) {
   constexpr int EPC = 16 / sizeof(T);
   const int V = c / EPC;
   const int nv = (V + G - 1) / G;
   const int rpb = 4 * (64 / G);
-  const int grid = std::min((rows + rpb - 1) / rpb, 512);
+  const int grid = std::min((rows + rpb - 1) / rpb, LNB_MAX_GRID);
 #define LNB_CASE(NVC)                                                                                      \
   if (nv <= NVC) {                                                                                         \
     hipLaunchKernelGGL((lnb_kernel<T, G, NVC>), dim3(grid), dim3(256), 0, s, (const T*)x, (const T*)dy, rows, c, \
-                       gamma, eps, (const T*)add, (T*)dx, dg, db);                                         \
-    return LDM_OK;                                                                                         \
+                       gamma, eps, (const T*)add, (T*)dx, part);                                           \
+    return lnb_params(part, grid, c, dg, db, acc, s);                                                      \
   }
   LNB_CASE(1) LNB_CASE(2) LNB_CASE(4) LNB_CASE(5) LNB_CASE(8)
 #undef LNB_CASE
@@ -801,15 +850,15 @@ int lnb_launch_g(const void* x, const void* dy, int rows, int c, const float* ga
 
 template <typename T>
 int lnb_launch(const void* x, const void* dy, int rows, int c, const float* gamma, float eps, const void* add,
-               void* dx, float* dg, float* db, hipStream_t s) {
+               void* dx, float* dg, float* db, int acc, float* part, hipStream_t s) {
   constexpr int EPC = 16 / sizeof(T);
   const int V = c / EPC;
   // the smallest lane group that keeps <= 4 chunks per lane (x, dy and two partial sets live
   // in registers per chunk)
-  if (V <= 8 * 4) return lnb_launch_g<T, 8>(x, dy, rows, c, gamma, eps, add, dx, dg, db, s);
-  if (V <= 16 * 4) return lnb_launch_g<T, 16>(x, dy, rows, c, gamma, eps, add, dx, dg, db, s);
-  if (V <= 32 * 4) return lnb_launch_g<T, 32>(x, dy, rows, c, gamma, eps, add, dx, dg, db, s);
-  return lnb_launch_g<T, 64>(x, dy, rows, c, gamma, eps, add, dx, dg, db, s);
+  if (V <= 8 * 4) return lnb_launch_g<T, 8>(x, dy, rows, c, gamma, eps, add, dx, dg, db, acc, part, s);
+  if (V <= 16 * 4) return lnb_launch_g<T, 16>(x, dy, rows, c, gamma, eps, add, dx, dg, db, acc, part, s);
+  if (V <= 32 * 4) return lnb_launch_g<T, 32>(x, dy, rows, c, gamma, eps, add, dx, dg, db, acc, part, s);
+  return lnb_launch_g<T, 64>(x, dy, rows, c, gamma, eps, add, dx, dg, db, acc, part, s);
 }
 
 size_t round16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -888,23 +937,35 @@ extern "C" int ldm_conv2d_wgrad(const ldm_wgrad_params* q, ldm_stream_t stream) 
   return LDM_OK;
 }
 
+constexpr int COLSUM_RCHUNK = 256;
+extern "C" size_t ldm_colsum_workspace_bytes(int rows, int c, int segments) {
+  if (rows <= 0 || c <= 0 || segments <= 0) return 0;
+  const int rps = rows / segments;
+  return (size_t)((rps + COLSUM_RCHUNK - 1) / COLSUM_RCHUNK) * segments * c * sizeof(float);
+}
+
 extern "C" int ldm_colsum(const void* x, int rows, int c, int segments, int geglu, float* out, int accumulate,
-                          int dtype, ldm_stream_t stream) {
-  if (!x || !out || rows <= 0 || c <= 0 || segments <= 0 || rows % segments) return LDM_ERR_ARG;
+                          void* workspace, int dtype, ldm_stream_t stream) {
+  if (!x || !out || !workspace || rows <= 0 || c <= 0 || segments <= 0 || rows % segments) return LDM_ERR_ARG;
   if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
   const int epc = dtype == LDM_F32 ? 4 : 8;
-  if (c % epc || !aligned16(x)) return LDM_ERR_ALIGN;
+  if (c % epc || !aligned16(x) || !aligned16(workspace)) return LDM_ERR_ALIGN;
   if (geglu && c % 32) return LDM_ERR_ARG;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (!accumulate && hipMemsetAsync(out, 0, (size_t)segments * c * sizeof(float), s) != hipSuccess)
-    return LDM_ERR_LAUNCH;
   const int rps = rows / segments;
-  const int rchunk = 256;
-  dim3 grid((c / epc + 63) / 64, (rps + rchunk - 1) / rchunk, segments);
+  const int chunks = (rps + COLSUM_RCHUNK - 1) / COLSUM_RCHUNK;
+  float* part = static_cast<float*>(workspace);
+  dim3 grid((c / epc + 63) / 64, chunks, segments);
   if (dtype == LDM_BF16)
-    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, c, rps, rchunk, geglu, out);
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)x, c, rps, COLSUM_RCHUNK, geglu,
+                       part);
   else
-    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)x, c, rps, rchunk, geglu, out);
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, s, (const float*)x, c, rps, COLSUM_RCHUNK, geglu,
+                       part);
+  LDM_CHECK_LAUNCH();
+  const int64_t width = (int64_t)segments * c;
+  hipLaunchKernelGGL(slab_reduce, dim3((unsigned)((width + 255) / 256)), dim3(256), 0, s, part, chunks, width, width,
+                     out, accumulate);
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
@@ -970,22 +1031,26 @@ extern "C" int ldm_group_norm_bwd(const void* x0, const void* x1, int c0, int c1
   return LDM_OK;
 }
 
+extern "C" size_t ldm_layer_norm_bwd_workspace_bytes(int rows, int c) {
+  if (rows <= 0 || c <= 0) return 0;
+  return (size_t)LNB_MAX_GRID * 2 * c * sizeof(float);
+}
+
 extern "C" int ldm_layer_norm_bwd(const void* x, const void* dy, int rows, int c, const float* gamma, float eps,
                                   const void* add_src, void* dx, float* dgamma, float* dbeta, int acc_params,
-                                  int dtype, ldm_stream_t stream) {
-  if (!x || !dy || !dx || !gamma || rows <= 0 || c <= 0) return LDM_ERR_ARG;
+                                  void* workspace, int dtype, ldm_stream_t stream) {
+  if (!x || !dy || !dx || !gamma || !workspace || rows <= 0 || c <= 0) return LDM_ERR_ARG;
   if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
   const int epc = dtype == LDM_F32 ? 4 : 8;
   if (c % epc) return LDM_ERR_ALIGN;
   if (c / epc > 64 * 8) return LDM_ERR_ARG;
   if (!aligned16(x) || !aligned16(dy) || !aligned16(dx) || (add_src && !aligned16(add_src))) return LDM_ERR_ALIGN;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (!acc_params) {
-    if (dgamma && hipMemsetAsync(dgamma, 0, (size_t)c * sizeof(float), s) != hipSuccess) return LDM_ERR_LAUNCH;
-    if (dbeta && hipMemsetAsync(dbeta, 0, (size_t)c * sizeof(float), s) != hipSuccess) return LDM_ERR_LAUNCH;
-  }
-  const int st = dtype == LDM_BF16 ? lnb_launch<bf16_t>(x, dy, rows, c, gamma, eps, add_src, dx, dgamma, dbeta, s)
-                                   : lnb_launch<float>(x, dy, rows, c, gamma, eps, add_src, dx, dgamma, dbeta, s);
+  float* part = static_cast<float*>(workspace);
+  const int acc = acc_params ? 1 : 0;
+  const int st = dtype == LDM_BF16
+                     ? lnb_launch<bf16_t>(x, dy, rows, c, gamma, eps, add_src, dx, dgamma, dbeta, acc, part, s)
+                     : lnb_launch<float>(x, dy, rows, c, gamma, eps, add_src, dx, dgamma, dbeta, acc, part, s);
   if (st != LDM_OK) return st;
   LDM_CHECK_LAUNCH();
   return LDM_OK;
@@ -1028,30 +1093,41 @@ extern "C" int ldm_sum_pool2(const void* x, int batch, int h_out, int w_out, int
 
 extern "C" int ldm_mse_loss(const void* pred, const float* target, const float* mask, const int64_t* t,
                             const float* weights, int num_weights, int batch, int ch, int hw, float grad_scale,
-                            void* dpred, double* loss_sum, int dtype, ldm_stream_t stream) {
-  if (!pred || !target || !loss_sum || batch <= 0 || ch <= 0 || hw <= 0) return LDM_ERR_ARG;
+                            void* dpred, double* loss_sum, void* workspace, int dtype, ldm_stream_t stream) {
+  if (!pred || !target || !loss_sum || !workspace || batch <= 0 || ch <= 0 || hw <= 0) return LDM_ERR_ARG;
   if (weights && (!t || num_weights <= 0)) return LDM_ERR_ARG;
   if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (hipMemsetAsync(loss_sum, 0, sizeof(double), s) != hipSuccess) return LDM_ERR_LAUNCH;
-  const int blocks = grid_for((int64_t)batch * ch * hw, 256 * 4, 1024);
+  double* part = static_cast<double*>(workspace);
+  const int blocks = grid_for((int64_t)batch * ch * hw, 256 * 4, DSUM_MAX_PARTS);
   if (dtype == LDM_BF16)
     hipLaunchKernelGGL(mse_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, (const bf16_t*)pred, target, mask, t, weights,
-                       num_weights, batch, ch, hw, grad_scale, (bf16_t*)dpred, loss_sum);
+                       num_weights, batch, ch, hw, grad_scale, (bf16_t*)dpred, part);
   else
     hipLaunchKernelGGL(mse_kernel<float>, dim3(blocks), dim3(256), 0, s, (const float*)pred, target, mask, t, weights,
-                       num_weights, batch, ch, hw, grad_scale, (float*)dpred, loss_sum);
+                       num_weights, batch, ch, hw, grad_scale, (float*)dpred, part);
+  LDM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dsum_final, dim3(1), dim3(256), 0, s, part, blocks, loss_sum, 0);
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
 
-extern "C" int ldm_sq_norm(const float* g, int64_t n, double* sum, int accumulate, ldm_stream_t stream) {
-  if (!g || !sum || n < 0) return LDM_ERR_ARG;
+extern "C" size_t ldm_reduce_workspace_bytes(void) { return DSUM_MAX_PARTS * sizeof(double); }
+
+extern "C" int ldm_sq_norm(const float* g, int64_t n, double* sum, int accumulate, void* workspace,
+                           ldm_stream_t stream) {
+  if (!g || !sum || !workspace || n < 0) return LDM_ERR_ARG;
   if (!aligned16(g)) return LDM_ERR_ALIGN;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (!accumulate && hipMemsetAsync(sum, 0, sizeof(double), s) != hipSuccess) return LDM_ERR_LAUNCH;
-  if (n == 0) return LDM_OK;
-  hipLaunchKernelGGL(sqnorm_kernel, dim3(grid_for(n / 4 + 1, 256 * 8, 2048)), dim3(256), 0, s, g, n, sum);
+  if (n == 0) {
+    if (!accumulate && hipMemsetAsync(sum, 0, sizeof(double), s) != hipSuccess) return LDM_ERR_LAUNCH;
+    return LDM_OK;
+  }
+  double* part = static_cast<double*>(workspace);
+  const int blocks = grid_for(n / 4 + 1, 256 * 8, DSUM_MAX_PARTS);
+  hipLaunchKernelGGL(sqnorm_kernel, dim3(blocks), dim3(256), 0, s, g, n, part);
+  LDM_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dsum_final, dim3(1), dim3(256), 0, s, part, blocks, sum, accumulate);
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }

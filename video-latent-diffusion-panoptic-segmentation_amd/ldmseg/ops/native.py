@@ -93,15 +93,18 @@ EXPORTS = {
                                _i, _vp]),
     "ldm_conv2d_wgrad_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(WgradParams)]),
     "ldm_conv2d_wgrad": (_i, [ctypes.POINTER(WgradParams), _vp]),
-    "ldm_colsum": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp]),
+    "ldm_colsum_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
+    "ldm_colsum": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _i, _vp]),
     "ldm_group_norm_bwd_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i, _i]),
     "ldm_group_norm_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp,
                                 _vp, _i, _vp, _i, _vp]),
-    "ldm_layer_norm_bwd": (_i, [_vp, _vp, _i, _i, _vp, _f, _vp, _vp, _vp, _vp, _i, _i, _vp]),
+    "ldm_layer_norm_bwd_workspace_bytes": (ctypes.c_size_t, [_i, _i]),
+    "ldm_layer_norm_bwd": (_i, [_vp, _vp, _i, _i, _vp, _f, _vp, _vp, _vp, _vp, _i, _vp, _i, _vp]),
     "ldm_geglu": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp]),
     "ldm_sum_pool2": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _i, _vp]),
-    "ldm_mse_loss": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _i, _vp]),
-    "ldm_sq_norm": (_i, [_vp, _i64, _vp, _i, _vp]),
+    "ldm_mse_loss": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, _i, _vp]),
+    "ldm_sq_norm": (_i, [_vp, _i64, _vp, _i, _vp, _vp]),
+    "ldm_reduce_workspace_bytes": (ctypes.c_size_t, []),
     "ldm_adamw": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i64, _f, _f, _f, _i, _vp, _f, _vp]),
     "ldm_panoptic_pixels": (_i, [_vp, _i, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp]),
     "ldm_panoptic_finalize": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _d, _i, _vp, _vp, _vp]),
@@ -624,8 +627,19 @@ def _gn_sources(x0, x1, batch, c0, c1, groups):
     return s0, s1, unit, slots
 
 
+GN_MAX_GROUPS = 64        # ldm_group_norm_ex: per-group statistics staged in LDS (gst[64])
+GN_MAX_CHANNELS = 2560    # GN_MAXC: the UNet's widest concat (csrc/norms.hip)
+
+
 def group_norm(x0, batch, hw, groups, gamma, beta, eps, act=ACT_NONE, x1=None, out=None):
-    """GroupNorm over NHWC [batch, hw, c0 (+c1)] -> contiguous NHWC [batch, hw, c0+c1]."""
+    """GroupNorm over NHWC [batch, hw, c0 (+c1)] -> contiguous NHWC [batch, hw, c0+c1].
+
+    The one-launch kernel stages <= 64 groups and <= 2560 channels in LDS (every SD-1.x UNet,
+    seg-VAE and PoseExpNet width fits); wider calls are refused here, before any launch."""
+    c_all = (x0.numel() + (0 if x1 is None else x1.numel())) // max(1, batch * hw)
+    if groups > GN_MAX_GROUPS or c_all > GN_MAX_CHANNELS or groups <= 0 or c_all % groups:
+        raise ValueError(f"group_norm: {groups} groups over {c_all} channels is outside the HIP kernel's range "
+                         f"(groups <= {GN_MAX_GROUPS} dividing C, C <= {GN_MAX_CHANNELS})")
     lib = load_library()
     _gpu(x0, x1, gamma, beta, out)
     _contig(x0, "x0")
@@ -915,8 +929,9 @@ def colsum(x, rows, c, segments=1, geglu=False, out=None, accumulate=False):
         accumulate = False
     elif out.numel() != segments * c or out.dtype != torch.float32 or not out.is_contiguous():
         raise ValueError("colsum: bad out")
-    _check(lib.ldm_colsum(_ptr(x), rows, c, segments, int(geglu), _ptr(out), int(accumulate), dtype_code(x.dtype),
-                          _stream(x)), "ldm_colsum")
+    ws = torch.empty(int(lib.ldm_colsum_workspace_bytes(rows, c, segments)), dtype=torch.uint8, device=x.device)
+    _check(lib.ldm_colsum(_ptr(x), rows, c, segments, int(geglu), _ptr(out), int(accumulate), _ptr(ws),
+                          dtype_code(x.dtype), _stream(x)), "ldm_colsum")
     return out
 
 
@@ -972,9 +987,10 @@ def layer_norm_bwd(x, dy, gamma, eps, add_src=None, dx=None, dgamma=None, dbeta=
     rows = x.numel() // C
     if dx is None:
         dx = torch.empty_like(x)
+    ws = torch.empty(int(lib.ldm_layer_norm_bwd_workspace_bytes(rows, C)), dtype=torch.uint8, device=x.device)
     _check(lib.ldm_layer_norm_bwd(_ptr(x), _ptr(dy), rows, C, _ptr(gamma), float(eps), _ptr(add_src), _ptr(dx),
-                                  _ptr(dgamma), _ptr(dbeta), int(acc_params), dtype_code(x.dtype), _stream(x)),
-           "ldm_layer_norm_bwd")
+                                  _ptr(dgamma), _ptr(dbeta), int(acc_params), _ptr(ws), dtype_code(x.dtype),
+                                  _stream(x)), "ldm_layer_norm_bwd")
     return dx
 
 
@@ -1034,9 +1050,10 @@ def mse_loss(pred, target, mask=None, t=None, weights=None, grad_scale=1.0, want
         weights = weights.float().contiguous()
     dpred = torch.empty_like(pred) if want_grad else None
     total = torch.empty((), dtype=torch.float64, device=pred.device)
+    ws = torch.empty(int(lib.ldm_reduce_workspace_bytes()), dtype=torch.uint8, device=pred.device)
     _check(lib.ldm_mse_loss(_ptr(pred), _ptr(target), _ptr(mask), _ptr(t), _ptr(weights),
                             0 if weights is None else weights.numel(), B, Cc, H * W, float(grad_scale), _ptr(dpred),
-                            _ptr(total), dtype_code(pred.dtype), _stream(pred)), "ldm_mse_loss")
+                            _ptr(total), _ptr(ws), dtype_code(pred.dtype), _stream(pred)), "ldm_mse_loss")
     return total, dpred
 
 
@@ -1048,7 +1065,8 @@ def sq_norm(g, out=None, accumulate=False):
     if out is None:
         out = torch.empty((), dtype=torch.float64, device=g.device)
         accumulate = False
-    _check(lib.ldm_sq_norm(_ptr(g), g.numel(), _ptr(out), int(accumulate), _stream(g)), "ldm_sq_norm")
+    ws = torch.empty(int(lib.ldm_reduce_workspace_bytes()), dtype=torch.uint8, device=g.device)
+    _check(lib.ldm_sq_norm(_ptr(g), g.numel(), _ptr(out), int(accumulate), _ptr(ws), _stream(g)), "ldm_sq_norm")
     return out
 
 
