@@ -433,6 +433,26 @@ int ldm_mse_loss(const void* pred, const float* target, const float* mask, const
 /* ldm_sq_norm — *sum (+)= sum g^2 over a flat fp32 buffer (fp64 accumulation, device). */
 int ldm_sq_norm(const float* g, int64_t n, double* sum, int accumulate, void* workspace, ldm_stream_t stream);
 
+/* ldm_repack — refresh packed weights in place from their fp32 source parameters (the training
+ * step, after each optimizer update), one launch over a device array of descriptors.  Chunk
+ * index space: descriptor i covers chunks [chunk0_i, chunk0_{i+1}) (chunk0 ascending, starting
+ * at 0), 8 destination elements per chunk.
+ *   mode 0: forward pack, bf16 dst[row0 + r][kpad], r < rows: dst[..][(ky*ks + kx)*cpad + c] =
+ *           W[r'][c][ky][kx] (W fp32 [co][ci][ks][ks]; r' = r, or the GEGLU 16-interleave's source
+ *           row when geglu; zero where r' >= co, c >= ci or the tap is past ks*ks)
+ *   mode 1: data-gradient pack (ldmseg packed_dgrad): dst[row0 + r][(ky*ks + kx)*cpad + c] =
+ *           W[c'][r][ks-1-ky][ks-1-kx], r < rows = ci, c' = c or its GEGLU source row, c < co
+ *   mode 2: fp32 vector dst[row0 + j] = src[j'] for j < rows (j' = j or its GEGLU source row,
+ *           co = the vector length).  rows = elements, chunks = ceil(rows / 8).
+ * f32: modes 0 / 1 write fp32 packs (the exact-fp32 compute path) instead of bf16. */
+typedef struct {
+  const float* src;
+  void* dst;
+  int64_t chunk0;
+  int rows, row0, kpad, co, ci, ks, cpad, mode, geglu, f32;
+} ldm_repack_desc;
+int ldm_repack(const ldm_repack_desc* descs, int ndesc, int64_t total_chunks, ldm_stream_t stream);
+
 /* Workspace of ldm_mse_loss / ldm_sq_norm: per-block fp64 partials, summed in a fixed order by a
  * second one-block pass (deterministic; no atomics). */
 size_t ldm_reduce_workspace_bytes(void);

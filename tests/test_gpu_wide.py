@@ -3,8 +3,8 @@ and torch fp32.
 
 It serves the large-N projections of diffusers' BasicTransformerBlock (the reference's UNet,
 /root/reference/ldmseg/models/unet.py:361-425, runs them through Transformer2DModel): the
-LayerNorm-folded QKV and GEGLU ff.net.0.  Its fp32 accumulation order over K (32-deep slices, one
-k32 MFMA step each, in K order) and its epilogue arithmetic are those of the 2-blocks-per-CU tile
+LayerNorm-folded QKV and GEGLU ff.net.0.  Its fp32 accumulation order over K (64-deep K tiles,
+two k32 MFMA steps each, in K order) and its epilogue arithmetic are those of the 2-blocks-per-CU tile
 kernel, so stored bf16 outputs must be bit-identical to the unsplit 128x128 tile path (forced plan:
 no split-K, no A-stationary kernel).  Against torch fp32 the bar is the conv tests' 2e-2 of the
 tensor scale.  Covered: ragged M (partial last tile, rows dropped by the store range check),

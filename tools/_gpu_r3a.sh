@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_wide.py tests/test_gpu_train_ops.py tests/test_gpu_train_full.py tests/test_gpu_train_step.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3a_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_wide.py tests/test_gpu_train_ops.py tests/test_gpu_train_full.py tests/test_gpu_train_step.py tests/test_gpu_repack.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r3a_tests.log 2>&1
 rc=$?
 tail -15 gpurun_out/r3a_tests.log
 if [ $rc -ne 0 ]; then exit $rc; fi

@@ -7,21 +7,19 @@
 // Why: the 128x160 two-blocks-per-CU tiles receive 36 KB of operands per 64-deep K tile for
 // 2.6 MFLOP (71 FLOP/B) and their main loops are bound by operand delivery into LDS.
 // A 256x320 tile receives 72 KB per 64 of K for 10.5 MFLOP (146 FLOP/B).  Such a tile needs all of
-// a CU (8 waves of 64x160 fp32 accumulators, a 144 KB LDS ring), so the launch is persistent: one
-// block per CU walks its tiles (XCD-contiguous ids, grouped raster) and the LDS-DMA stream never
-// stops at a tile boundary.  Measured on the first (two-slot, 64-deep) form: with the MFMAs removed
-// the kernel ran exactly as long, with the loads removed 40 % shorter — the main loop waited on
-// the single K tile in flight (~28 GB/s per CU at 80 % L2 hits).  So the ring holds four 32-deep
-// K slices and keeps three in flight (108 KB) while one is multiplied.
+// a CU (8 waves of 64x160 fp32 accumulators, a 144 KB two-slot LDS ring), so the launch is
+// persistent: one block per CU walks its tiles (XCD-contiguous ids, grouped raster) and the LDS-DMA
+// stream never stops at a tile boundary — the next tile's first K tile is in flight while the
+// current tile's epilogue runs.  Tuning log: a four-slot ring of 32-deep slices
+// (64-B operand rows) kept more bytes in flight but ran 10-30 % slower: every wave instruction then
+// fetches 16 half cache lines.
 //
-// The epilogue runs from registers and never touches the ring: the next tile's first slices stream
-// in while it stores.  Per-tile column constants (bias, LayerNorm-fold column sums) and row
-// constants (LayerNorm-fold row statistics) arrive with the tile's first slice by LDS-DMA into a
-// small double-buffered scratch, so no compiler-visible global load is left in the kernel — such a
-// load would make hipcc wait vmcnt(0) and drain the prefetch.  Every wait on the DMA stream is a
-// counted vmcnt computed from the exact per-wave instruction counts (stores included: they are
-// issued as raw buffer stores, out-of-range rows dropped by the hardware range check, so their
-// count is fixed).
+// The epilogue runs from registers and never touches the ring.  Per-tile column constants (bias,
+// LayerNorm-fold column sums) and row constants (LayerNorm-fold row statistics) arrive with the
+// tile's first K tile by LDS-DMA into a small double-buffered scratch, so no compiler-visible global
+// load is left in the kernel (hipcc would wait vmcnt(0) for it and drain the prefetch).  The only
+// wait that must not drain is the one after an epilogue: its stores are raw buffer stores (rows
+// past M dropped by the range check), so their count per lane is fixed and the wait is counted.
 //   NHWC (QKV): act(acc + bias) with the LayerNorm fold, packed to bf16; lanes (g, lr) and
 //     (g ^ 1, lr) exchange one fragment's halves so every lane stores 16 B (8 channels).
 //   GEGLU: h * gelu(g) from the hidden / gate fragment pair that shares a lane, 8-B stores.
@@ -37,36 +35,17 @@ constexpr int BN = 320;
 constexpr int WM = 64, WN = 160;    // wave tile: 4 waves along M, 2 along N
 constexpr int FM = WM / 16;         // 4 fragments along M
 constexpr int FN = WN / 16;         // 10 along N
-constexpr int KS = 32;              // K per ring slice (64 B per operand row)
-constexpr int NSLOT = 4;            // ring slots: three slices in flight while one is multiplied
-constexpr int SLOT_U4 = (BM + BN) * 4;      // uint4 per slot (36 KB)
-constexpr int A_INS = BM / 16 / 8;          // A DMA instructions per wave and slice (16 rows each)
-constexpr int B_INS_TOT = BN / 16;          // 20 B instructions per slice over 8 waves: 3 or 2
+constexpr int KS = 64;              // K per ring slot (128 B per operand row)
+constexpr int NSLOT = 2;
+constexpr int SLOT_U4 = (BM + BN) * 8;      // uint4 per slot (72 KB)
+constexpr int A_INS = BM / 8 / 8;           // A DMA instructions per wave and K tile (8 rows each): 4
+constexpr int B_INS = BN / 8 / 8;           // 5
 // scratch floats per tile: bias [320] at 0, c1 [320] at 512, rows [256][2] at 1024 — six wave DMA
 // instructions of 256 floats, each from one source (the buffer descriptor is wave-uniform)
 constexpr int SCR_F = 1536;
 constexpr int SCR_C1 = 512, SCR_ROW = 1024;
 constexpr int NST = FM * FN / 2;            // epilogue store instructions per lane (20)
-// physical 16-B chunk of logical chunk c in 64-B row r: conflict-free ds_read_b128 for the
-// 16x16x32 fragment lanes (rows lr = 0..15, chunks g): h(r) = -(r >> 2) mod 4
-__device__ __forceinline__ int swz4(int r, int c) { return c ^ ((4 - ((r >> 2) & 3)) & 3); }
 }  // namespace wide
-
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate is an instruction field)
-__device__ __forceinline__ void wait_vm(int n) {
-  switch (n) {
-#define LDM_WV(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    LDM_WV(0) LDM_WV(1) LDM_WV(2) LDM_WV(3) LDM_WV(4) LDM_WV(5) LDM_WV(6) LDM_WV(7) LDM_WV(8) LDM_WV(9)
-    LDM_WV(10) LDM_WV(11) LDM_WV(12) LDM_WV(13) LDM_WV(14) LDM_WV(15) LDM_WV(16) LDM_WV(17) LDM_WV(18)
-    LDM_WV(19) LDM_WV(20) LDM_WV(21) LDM_WV(22) LDM_WV(23) LDM_WV(24) LDM_WV(25) LDM_WV(26) LDM_WV(27)
-    LDM_WV(28) LDM_WV(29) LDM_WV(30) LDM_WV(31) LDM_WV(32) LDM_WV(33) LDM_WV(34) LDM_WV(35) LDM_WV(36)
-    LDM_WV(37) LDM_WV(38) LDM_WV(39) LDM_WV(40) LDM_WV(41) LDM_WV(42) LDM_WV(43) LDM_WV(44) LDM_WV(45)
-    LDM_WV(46) LDM_WV(47) LDM_WV(48) LDM_WV(49) LDM_WV(50) LDM_WV(51) LDM_WV(52) LDM_WV(53) LDM_WV(54)
-    LDM_WV(55) LDM_WV(56) LDM_WV(57) LDM_WV(58) LDM_WV(59) LDM_WV(60) LDM_WV(61) LDM_WV(62)
-#undef LDM_WV
-    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
-  }
-}
 
 // GEGLU: the epilogue form (one instantiation per form)
 template <bool GEGLU>
@@ -78,11 +57,12 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   const int wm = wave >> 1, wn = wave & 1;
   const int lr = lane & 15, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  // DMA lane geometry: one wave instruction = 16 rows x 64 B; lane -> row lane >> 2, chunk lane & 3
-  const int drow = lane >> 2;
-  const int dchunk = (lane & 3) ^ ((4 - ((drow >> 2) & 3)) & 3);   // source-side swizzle
-  const int b_ins = (wv + 16 < B_INS_TOT) ? 3 : 2;                  // this wave's B instructions
-  const int scr_ins = wv < 6 ? 1 : 0;                               // scratch DMA (tile's first slice)
+  // DMA lane geometry: one wave instruction = 8 rows x 128 B; wave wv's instruction i covers rows
+  // 8 (wv + 8 i) + (lane >> 3); the lane at chunk position lane & 7 fetches logical chunk
+  // (lane & 7) ^ ((row >> 1) & 7) (source-side swizzle; (row >> 1) & 7 does not depend on i)
+  const int drow = lane >> 3;
+  const int dchunk = (lane & 7) ^ (((8 * wv + drow) >> 1) & 7);
+  const int scr_ins = wv < 6 ? 1 : 0;                               // scratch DMA (tile's first K tile)
 
   const int tiles_m = (p.M + BM - 1) / BM;
   const int ntiles = tiles_m * p.tiles_n;
@@ -120,36 +100,35 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
     m0 = tm * BM;
     n0 = tn * BN;
   };
-  // DMA instructions this wave issues for slice s
-  auto per = [&](int s) { return A_INS + b_ins + ((s % nks) == 0 ? scr_ins : 0); };
-  // slice s of this block's stream = K slice (s mod nks) of its tile s / nks
+  // step s of this block's stream = K tile (s mod nks) of its tile s / nks
   auto issue = [&](int s) {
+#ifdef LDM_ABL_NO_LOADS
+    return;
+#endif
     const int r = s / nks, kt = s - r * nks;
     int m0, n0;
     coords(r, m0, n0);
-    const unsigned abase = lds0 + (unsigned)((s & (NSLOT - 1)) * SLOT_U4 * 16);
-    const unsigned bbase = abase + BM * 64;
+    const unsigned abase = lds0 + (unsigned)((s & 1) * SLOT_U4 * 16);
+    const unsigned bbase = abase + BM * 128;
     const int k0 = kt * KS;
     const int sel = (p.c1 > 0 && k0 >= p.c0) ? 1 : 0;   // concat boundary is slice aligned (host)
     const int cs = sel ? p.c1 : p.c0;
     const int choff = (sel ? k0 - p.c0 : k0) + dchunk * 8;
 #pragma unroll
     for (int i = 0; i < A_INS; ++i) {
-      const int q = wv + 8 * i;                         // instruction index: rows 16q .. 16q + 15
-      const int m = m0 + 16 * q + drow;
+      const int q = wv + 8 * i;                         // instruction index: rows 8q .. 8q + 7
+      const int m = m0 + 8 * q + drow;
       const int off = m < p.M ? (m * cs + choff) * 2 : kOOB;
-      const unsigned dst = __builtin_amdgcn_readfirstlane(abase + q * 16 * 64);
+      const unsigned dst = __builtin_amdgcn_readfirstlane(abase + q * 8 * 128);
       if (sel) dma16(ra1, off, dst);
       else dma16(ra0, off, dst);
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < B_INS; ++i) {
       const int q = wv + 8 * i;
-      if (q < B_INS_TOT) {                              // wave-uniform
-        const int n = n0 + 16 * q + drow;
-        const int off = n < p.n ? (n * p.kpad + k0 + dchunk * 8) * 2 : kOOB;
-        dma16(rw, off, __builtin_amdgcn_readfirstlane(bbase + q * 16 * 64));
-      }
+      const int n = n0 + 8 * q + drow;
+      const int off = n < p.n ? (n * p.kpad + k0 + dchunk * 8) * 2 : kOOB;
+      dma16(rw, off, __builtin_amdgcn_readfirstlane(bbase + q * 8 * 128));
     }
     if (kt == 0 && scr_ins) {
       // instruction wv: 0, 1 bias [256 wv, +256); 2, 3 c1; 4, 5 rows [m0 + 128 (wv - 4), +128)
@@ -168,33 +147,38 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   f32x4_t acc[FM][FN];
   auto compute = [&](int slot) {
     const uint4* As = smem + slot * SLOT_U4;
-    const uint4* Bs = As + BM * 4;
-    Frag8<bf16_t> af[FM];
+    const uint4* Bs = As + BM * 8;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int r = wm * WM + i * 16 + lr;
-      af[i].v = As[r * 4 + swz4(r, g)];
-    }
+    for (int ks = 0; ks < 2; ++ks) {
+      Frag8<bf16_t> af[FM];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int r = wn * WN + j * 16 + lr;
-      Frag8<bf16_t> bf;
-      bf.v = Bs[r * 4 + swz4(r, g)];
-#ifdef LDM_ABL_NO_MFMA   // ablation build: fragments read from LDS, no MFMA issued
-      asm volatile("" ::"v"(bf.v.x), "v"(bf.v.w));
-      if (j == 0) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[i].v.x), "v"(af[i].v.w));
+      for (int i = 0; i < FM; ++i) {
+        const int r = wm * WM + i * 16 + lr;
+        af[i].v = As[r * 8 + swz(r, ks * 4 + g)];
       }
-      continue;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int r = wn * WN + j * 16 + lr;
+        Frag8<bf16_t> bf;
+        bf.v = Bs[r * 8 + swz(r, ks * 4 + g)];
+#ifdef LDM_ABL_NO_MFMA   // ablation build: fragments read from LDS, no MFMA issued
+        asm volatile("" ::"v"(bf.v.x), "v"(bf.v.w));
+        if (j == 0) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i) asm volatile("" ::"v"(af[i].v.x), "v"(af[i].v.w));
+        }
+        continue;
 #endif
 #pragma unroll
-      for (int i = 0; i < FM; ++i) mma_k32(acc[i][j], bf, af[i]);
+        for (int i = 0; i < FM; ++i) mma_k32(acc[i][j], bf, af[i]);
+      }
+      // keep the second k32 step's fragment reads from being hoisted beside the first step's
+      // (160 accumulator registers leave no room for two steps' fragments)
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  int issued = 0;
-  for (; issued < total && issued < NSLOT - 1; ++issued) issue(issued);
+  if (total > 0) issue(0);
   int s = 0;
   for (int r = 0; r < my_tiles; ++r) {
     int m0, n0;
@@ -204,16 +188,14 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < nks; ++kt, ++s) {
-      // slice s landed for this wave: the younger slices (and the previous tile's epilogue stores,
-      // issued after them) may stay in flight
-      int younger = 0;
-      for (int x = s + 1; x < issued; ++x) younger += per(x);
-      if (kt == 0 && r > 0) younger += NST;
-      wait_vm(younger);
-      // every wave's part of slice s is in LDS, and every wave is done with slot (s - 1) & 3
+      // K tile s landed for this wave; after an epilogue its NST stores (issued after the DMA) may
+      // stay in flight
+      if (kt == 0 && r > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // every wave's part of tile s is in LDS, and every wave is done with slot (s + 1) & 1
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (issued < total && issued <= s + NSLOT - 1) issue(issued++);
-      compute(s & (NSLOT - 1));
+      if (s + 1 < total) issue(s + 1);
+      compute(s & 1);
     }
     // ---- epilogue from registers; this tile's scratch landed with its first slice
     const float* sbias = scr + (r & 1) * SCR_F;
@@ -304,15 +286,15 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
 
 namespace ldm_igemm {
 
-// legal: bf16 1x1 GEMM (one source, or a concat whose boundary is 32-channel aligned), N a
+// legal: bf16 1x1 GEMM (one source, or a concat whose boundary is 64-channel aligned), N a
 // multiple of 320, NHWC (bias / activation / LayerNorm fold) or GEGLU (bias / LayerNorm fold); no
 // residual, row or GroupNorm statistics, time embedding, split-K or fp32 output
 static int g_wide_mode = 0;   // tuning hook: 0 planner, 1 never, 2 whenever legal
 bool wide_legal(const ldm_conv_params* q, int es, bool mixed) {
   const auto a16 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; };
   if (es != 2 || mixed || q->ksize != 1 || q->stride != 1 || q->upsample || q->pad_mode != 0) return false;
-  // >= 4 K slices per tile: a tile's scratch buffer is rewritten only after its epilogue
-  if (q->c0 % wide::KS || q->c1 % wide::KS || q->kpad % wide::KS || q->kpad < 4 * wide::KS || q->n % wide::BN)
+  // >= 2 K tiles per tile: a tile's scratch buffer is rewritten only after its epilogue
+  if (q->c0 % wide::KS || q->c1 % wide::KS || q->kpad % wide::KS || q->kpad < 2 * wide::KS || q->n % wide::BN)
     return false;
   if (q->out_layout != LDM_OUT_NHWC && q->out_layout != LDM_OUT_GEGLU) return false;
   if (q->out_f32 || q->temb || q->residual || q->row_stats || q->gn_partial) return false;

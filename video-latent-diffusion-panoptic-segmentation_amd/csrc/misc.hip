@@ -382,3 +382,83 @@ extern "C" int ldm_softmax_rows(const float* s, int rows, int n, int stride, flo
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
+
+// ======================================================================================
+// Packed-weight refresh (the training step's per-iteration repack, trainers/ldm.py): after the
+// fused AdamW updates the fp32 master weights, every bf16 [n][kpad] forward pack, every flipped /
+// transposed data-gradient pack and every concatenated / interleaved fp32 bias vector is rewritten
+// in place from its source parameters by ONE launch over a descriptor table — instead of ~1200
+// torch permute / pad / cast kernels per iteration (profiles/r02d_train_kernel_stats.csv).
+// Layouts are those of ldmseg.ops.native.PackedConv and models.unet_train.packed_dgrad.
+// ======================================================================================
+namespace {
+__device__ __forceinline__ int geglu_src_row(int p, int half) {   // packed (interleaved) row -> source row
+  const int blk = p >> 5, w = p & 31;
+  return w < 16 ? blk * 16 + w : half + blk * 16 + (w - 16);
+}
+
+__global__ __launch_bounds__(256) void repack_kernel(const ldm_repack_desc* __restrict__ d, int nd, int64_t total) {
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= total) return;
+  int lo = 0, hi = nd - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].chunk0 <= q) lo = mid; else hi = mid - 1;
+  }
+  const ldm_repack_desc e = d[lo];
+  const int64_t local = q - e.chunk0;
+  const float* src = e.src;
+  if (e.mode == 2) {                                   // fp32 vector [row0 + j] = src[perm j]
+    float* dst = static_cast<float*>(e.dst);
+    for (int k = 0; k < 8; ++k) {
+      const int j = (int)(local * 8) + k;
+      if (j >= e.rows) break;
+      dst[e.row0 + j] = src[e.geglu ? geglu_src_row(j, e.co >> 1) : j];
+    }
+    return;
+  }
+  const int cpk = e.kpad >> 3;                         // 8-element chunks per packed row
+  const int r = (int)(local / cpk);
+  const int k0 = (int)(local - (int64_t)r * cpk) * 8;
+  const int taps = e.ks * e.ks;
+  float v8[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int kk = k0 + k;
+    const int tap = kk / e.cpad, c = kk - tap * e.cpad;
+    float v = 0.f;
+    if (tap < taps) {
+      const int ky = tap / e.ks, kx = tap - ky * e.ks;
+      if (e.mode == 0) {                               // W[co][ci][ky][kx] -> [co][(ky, kx, ci)]
+        const int co = e.geglu ? geglu_src_row(r, e.co >> 1) : r;
+        if (co < e.co && c < e.ci) v = src[(((int64_t)co * e.ci + c) * e.ks + ky) * e.ks + kx];
+      } else {                                         // W[co][ci][2-ky][2-kx] -> [ci][(ky, kx, co)]
+        const int co = e.geglu ? geglu_src_row(c, e.co >> 1) : c;
+        if (c < e.co && r < e.ci)
+          v = src[(((int64_t)co * e.ci + r) * e.ks + (e.ks - 1 - ky)) * e.ks + (e.ks - 1 - kx)];
+      }
+    }
+    v8[k] = v;
+  }
+  if (e.f32) {                                         // fp32 packs (the exact-fp32 compute path)
+    float* dst = static_cast<float*>(e.dst) + (int64_t)(e.row0 + r) * e.kpad + k0;
+    reinterpret_cast<float4*>(dst)[0] = make_float4(v8[0], v8[1], v8[2], v8[3]);
+    reinterpret_cast<float4*>(dst)[1] = make_float4(v8[4], v8[5], v8[6], v8[7]);
+    return;
+  }
+  bf16_t h[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) h[k] = f2bf(v8[k]);
+  bf16_t* dst = static_cast<bf16_t*>(e.dst);
+  *reinterpret_cast<uint4*>(dst + (int64_t)(e.row0 + r) * e.kpad + k0) = *reinterpret_cast<const uint4*>(h);
+}
+}  // namespace
+
+extern "C" int ldm_repack(const ldm_repack_desc* descs, int ndesc, int64_t total_chunks, ldm_stream_t stream) {
+  if (!descs || ndesc <= 0 || total_chunks <= 0) return LDM_ERR_ARG;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(repack_kernel, dim3((unsigned)((total_chunks + 255) / 256)), dim3(256), 0, s, descs, ndesc,
+                     total_chunks);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}

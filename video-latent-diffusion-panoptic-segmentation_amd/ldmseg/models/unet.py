@@ -363,7 +363,20 @@ class UNet(nn.Module):
 
     # ------------------------------------------------------------ packed-weight plan
     def _signature(self):
-        return (self.compute_dtype, self.device) + tuple((p.data_ptr(), p._version) for p in self.parameters())
+        return (self.compute_dtype, self.device, self.ln_fold) + tuple((p.data_ptr(), p._version)
+                                                                       for p in self.parameters())
+
+    @staticmethod
+    def _pk(weights, biases, dt, **kw):
+        """PackedConv of the row-concatenation of ``weights`` (+ concatenated ``biases``), recording
+        its source parameters so models.repack.PackRefresher can rewrite it in place after an
+        optimizer update (ldm_repack) instead of re-running this packing."""
+        w = weights[0] if len(weights) == 1 else torch.cat(weights)
+        bs = [b for b in biases if b is not None]
+        b = None if not bs else (bs[0] if len(bs) == 1 else torch.cat(bs))
+        pc = K.PackedConv(w, b, dt, **kw)
+        pc.src_w, pc.src_b = list(weights), bs
+        return pc
 
     def prepare(self, force=False):
         """(Re)pack every weight for the HIP kernels; cached until a parameter changes."""
@@ -377,7 +390,7 @@ class UNet(nn.Module):
         P = {}
         cin = self.conv_in.in_channels
         cin_pad = (cin + 15) // 16 * 16
-        P["conv_in"] = K.PackedConv(self.conv_in.weight, self.conv_in.bias, dt, cin_pad=cin_pad)
+        P["conv_in"] = self._pk([self.conv_in.weight], [self.conv_in.bias], dt, cin_pad=cin_pad)
         P["cin_pad"] = cin_pad
         P["freqs"] = self.time_proj.frequencies(self.device)
         te = self.time_embedding
@@ -391,27 +404,27 @@ class UNet(nn.Module):
             bs.append(r.time_emb_proj.bias)
             P[id(r), "temb_off"] = off
             off += r.out_channels
-        P["temb_proj"] = K.PackedConv(torch.cat(ws), torch.cat(bs), dt)
+        P["temb_proj"] = self._pk(ws, bs, dt)
         P["temb_total"] = off
         for r in resnets:
             P[id(r)] = dict(
                 n1=(f32(r.norm1.weight), f32(r.norm1.bias)), n2=(f32(r.norm2.weight), f32(r.norm2.bias)),
-                c1=K.PackedConv(r.conv1.weight, r.conv1.bias, dt), c2=K.PackedConv(r.conv2.weight, r.conv2.bias, dt),
-                sc=None if r.conv_shortcut is None else K.PackedConv(r.conv_shortcut.weight, r.conv_shortcut.bias, dt),
+                c1=self._pk([r.conv1.weight], [r.conv1.bias], dt), c2=self._pk([r.conv2.weight], [r.conv2.bias], dt),
+                sc=None if r.conv_shortcut is None else self._pk([r.conv_shortcut.weight], [r.conv_shortcut.bias], dt),
                 off=P[id(r), "temb_off"])
         for t in [m for m in self.modules() if isinstance(m, Transformer2DModel)]:
             tb = t.transformer_blocks[0]
             a1 = tb.attn1
             d = dict(norm=(f32(t.norm.weight), f32(t.norm.bias)),
-                     proj_in=K.PackedConv(t.proj_in.weight, t.proj_in.bias, dt),
-                     proj_out=K.PackedConv(t.proj_out.weight, t.proj_out.bias, dt),
+                     proj_in=self._pk([t.proj_in.weight], [t.proj_in.bias], dt),
+                     proj_out=self._pk([t.proj_out.weight], [t.proj_out.bias], dt),
                      ln1=(f32(tb.norm1.weight), f32(tb.norm1.bias)), ln3=(f32(tb.norm3.weight), f32(tb.norm3.bias)),
-                     qkv=K.PackedConv(torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight]), None, dt),
-                     out1=K.PackedConv(a1.to_out[0].weight, a1.to_out[0].bias, dt),
+                     qkv=self._pk([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight], [], dt),
+                     out1=self._pk([a1.to_out[0].weight], [a1.to_out[0].bias], dt),
                      heads=a1.heads, dim_head=a1.dim_head,
-                     ff1=K.PackedConv(tb.ff.net[0].proj.weight, tb.ff.net[0].proj.bias, dt, geglu=True),
-                     ff2=K.PackedConv(tb.ff.net[2].weight, tb.ff.net[2].bias, dt), attn2=None)
-            if dt == torch.bfloat16:
+                     ff1=self._pk([tb.ff.net[0].proj.weight], [tb.ff.net[0].proj.bias], dt, geglu=True),
+                     ff2=self._pk([tb.ff.net[2].weight], [tb.ff.net[2].bias], dt), attn2=None)
+            if dt == torch.bfloat16 and self.ln_fold:
                 # norm1 -> QKV and norm3 -> ff.net.0 as single GEMMs on the raw rows (the producers,
                 # proj_in and to_out, sum each row's statistics in their epilogues)
                 d["qkv_ln"] = K.packed_ln_fold(torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight]), None,
@@ -428,9 +441,9 @@ class UNet(nn.Module):
             P[id(t)] = d
         for m in self.modules():
             if isinstance(m, (Downsample2D, Upsample2D)):
-                P[id(m)] = K.PackedConv(m.conv.weight, m.conv.bias, dt)
+                P[id(m)] = self._pk([m.conv.weight], [m.conv.bias], dt)
         P["out_norm"] = (f32(self.conv_norm_out.weight), f32(self.conv_norm_out.bias))
-        P["conv_out"] = K.PackedConv(self.conv_out.weight, self.conv_out.bias, dt)
+        P["conv_out"] = self._pk([self.conv_out.weight], [self.conv_out.bias], dt)
         P["resnets"] = resnets
         self._plan, self._plan_key = P, key
         self._dplan = None
@@ -457,6 +470,7 @@ class UNet(nn.Module):
             D[id(t.proj_in)] = packed_dgrad(t.proj_in.weight, dt)
             D[id(t.proj_out)] = packed_dgrad(t.proj_out.weight, dt)
             D[id(a1)] = packed_dgrad(torch.cat([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight]), dt)
+            D[id(a1)].dg_src = ([a1.to_q.weight, a1.to_k.weight, a1.to_v.weight], False)
             D[id(a1.to_out[0])] = packed_dgrad(a1.to_out[0].weight, dt)
             D[id(tb.ff.net[0].proj)] = packed_dgrad(tb.ff.net[0].proj.weight, dt, geglu=True)
             D[id(tb.ff.net[2])] = packed_dgrad(tb.ff.net[2].weight, dt)
@@ -469,6 +483,7 @@ class UNet(nn.Module):
                            device=self.conv_out.weight.device)
         wpad[:co] = self.conv_out.weight.detach()
         P["conv_out_t"] = K.PackedConv(wpad, None, dt)
+        P["conv_out_t"].src_w, P["conv_out_t"].src_b = [self.conv_out.weight], []   # rows co..7 stay zero
         self._dplan = D
         return D
 
@@ -506,8 +521,10 @@ class UNet(nn.Module):
 
     def set_ln_fold(self, enabled=True):
         """bf16 inference: fold norm1 / norm3 into the QKV / ff.net.0 GEMMs (default on); off runs
-        the separate LayerNorm kernels (A/B, and the form the training path differentiates)."""
+        the separate LayerNorm kernels (A/B, and the form the training path differentiates — the
+        training step turns it off, so its packs can be refreshed in place by ldm_repack)."""
         self._ln_fold = bool(enabled)
+        self._plan = self._plan_key = self._dplan = None
 
     def _transformer(self, P, t, x, B, H, W, ehs):
         p = P[id(t)]

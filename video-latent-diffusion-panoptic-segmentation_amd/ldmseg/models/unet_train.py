@@ -44,7 +44,9 @@ def packed_dgrad(weight, dtype, geglu=False, cin_pad=None):
         wh, wg = w[:half].reshape(half // 16, 16, *w.shape[1:]), w[half:].reshape(half // 16, 16, *w.shape[1:])
         w = torch.stack([wh, wg], dim=1).reshape(cout, *w.shape[1:])
     wt = w.flip(-1, -2).transpose(0, 1).contiguous()
-    return K.PackedConv(wt, None, dtype, cin_pad=cin_pad)
+    pc = K.PackedConv(wt, None, dtype, cin_pad=cin_pad)
+    pc.dg_src = (weight, geglu)            # models.repack.PackRefresher (ldm_repack mode 1)
+    return pc
 
 
 class _Grads:

@@ -105,6 +105,7 @@ EXPORTS = {
     "ldm_mse_loss": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i, _i, _i, _f, _vp, _vp, _vp, _i, _vp]),
     "ldm_sq_norm": (_i, [_vp, _i64, _vp, _i, _vp, _vp]),
     "ldm_reduce_workspace_bytes": (ctypes.c_size_t, []),
+    "ldm_repack": (_i, [_vp, _i, _i64, _vp]),
     "ldm_adamw": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _i64, _f, _f, _f, _i, _vp, _f, _vp]),
     "ldm_panoptic_pixels": (_i, [_vp, _i, _i, _i, _i, _f, _i, _vp, _vp, _vp, _vp]),
     "ldm_panoptic_finalize": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _d, _i, _vp, _vp, _vp]),
@@ -1068,6 +1069,14 @@ def sq_norm(g, out=None, accumulate=False):
     ws = torch.empty(int(lib.ldm_reduce_workspace_bytes()), dtype=torch.uint8, device=g.device)
     _check(lib.ldm_sq_norm(_ptr(g), g.numel(), _ptr(out), int(accumulate), _ptr(ws), _stream(g)), "ldm_sq_norm")
     return out
+
+
+def repack(table, ndesc, total_chunks, device):
+    """ldm_repack over a device byte table of ndesc ldm_repack_desc records (models/repack.py)."""
+    lib = load_library()
+    _gpu(table)
+    _check(lib.ldm_repack(_ptr(table), int(ndesc), int(total_chunks),
+                          ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)), "ldm_repack")
 
 
 def adamw(param, grad, exp_avg, exp_avg_sq, segments, nseg, step, beta1=0.9, beta2=0.999, eps=1e-8, sqsum=None,

@@ -35,6 +35,7 @@ import torch
 import torch.distributed as dist
 import torch.nn as nn
 
+from ..models.repack import PackRefresher
 from ..models.unet import ResnetBlock2D
 from ..models.unet_train import UNetTrainGraph
 from ..ops import native as K
@@ -83,6 +84,10 @@ class LDMTrainStep:
                  eps=1e-8, clip_grad=3.0, lr_factor_func=None, self_condition=False, min_noise_level=0,
                  compute_dtype=torch.bfloat16, bucket_mb=100, group=None, seed=None, zero_redundancy=False):
         self.unet, self.sched = unet, scheduler
+        # the training forward differentiates separate LayerNorms; with the fold off every pack is a
+        # plain layout of its parameters, refreshed in place after each update (models/repack.py)
+        unet.set_ln_fold(False)
+        self.refresher = PackRefresher(unet)
         self.self_condition = self_condition
         self.min_noise_level = min_noise_level
         self.clip_grad = float(clip_grad)
@@ -348,4 +353,4 @@ class LDMTrainStep:
                     max_norm=self.clip_grad if self.clip_grad > 0 else 0.0)
         if self.zero:
             self._gather_parameters()
-        self.unet.invalidate_packed()
+        self.refresher.run()                               # packs rewritten in place (ldm_repack)
