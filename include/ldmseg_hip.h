@@ -92,15 +92,18 @@ typedef struct {
                               so the row tiles of one batch are spread over the slots */
   /* LayerNorm folded into 1x1 GEMMs (bf16, NHWC or GEGLU output, no time embedding, no
    * gn_partial; the transformer block's norm1 -> QKV and norm3 -> ff.net.0, unet.py:83-105):
-   *   row_stats  optional OUTPUT: [M][2] fp32 (sum, sumsq) of each stored output row, ADDED
-   *              atomically (zero it first) — the statistics of the next LayerNorm's input;
+   *   row_stats  optional OUTPUT: [M][2] fp64 (sum, sumsq) of each stored output row, ADDED
+   *              atomically (zero it first) — the statistics of the next LayerNorm's input.  The
+   *              per-tile partials are fp32 and their fp64 sum is exact, so the result does not
+   *              depend on the order the tiles land in (run-to-run deterministic), and the fold's
+   *              E[x^2] - mean^2 is taken in fp64 (no cancellation for rows with |mean| >> std);
    *   ln_rows    optional INPUT: [M][2] (sum, sumsq) of each row of a0 (a row_stats), with
    *              ln_c1 [n] = sum_k W'[n][k] (W' = W diag(gamma), the packed weight) and bias =
    *              W beta + b: out = rstd (acc - mean c1) + bias = Linear(LayerNorm(a0)), where
    *              mean = sum * ln_inv_k, rstd = 1 / sqrt(sumsq * ln_inv_k - mean^2 + ln_eps).
    * Either forces an unsplit 1x1 tile plan of the 2-blocks-per-CU kernel. */
-  float* row_stats;
-  const float* ln_rows;
+  double* row_stats;
+  const double* ln_rows;
   const float* ln_c1;
   float ln_inv_k;
   float ln_eps;

@@ -50,7 +50,7 @@ def test_ars_linear_residual_rowstats(M, N, act, ars_mode):
     res = torch.randn(M, N).to(DEV, BF)
 
     def run():
-        rows = torch.zeros(M, 2, device=DEV)
+        rows = torch.zeros(M, 2, device=DEV, dtype=torch.float64)
         y = K.linear(pc, x, residual=res, row_stats=rows, act=act)
         return y, rows
     (y0, r0), (y1, r1) = both(run, ars_mode)
@@ -63,7 +63,7 @@ def test_ars_linear_residual_rowstats(M, N, act, ars_mode):
         ref = ref + res.float()
     assert rel_err(y1, ref) < 2e-2
     hf = y1.float()
-    assert torch.allclose(r1[:, 0], hf.sum(1), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(r1[:, 0], hf.double().sum(1), rtol=1e-4, atol=1e-2)
 
 
 @pytest.mark.parametrize("M", [512, 8192 + 256 + 13])
@@ -77,7 +77,7 @@ def test_ars_in_place_residual(M, ars_mode):
 
     def run():
         h = h0.clone()
-        rows = torch.zeros(M, 2, device=DEV)
+        rows = torch.zeros(M, 2, device=DEV, dtype=torch.float64)
         K.linear(pc, a, residual=h, out=h, row_stats=rows)
         return h, rows
     (y0, r0), (y1, r1) = both(run, ars_mode)
@@ -91,7 +91,7 @@ def test_ars_layernorm_fold_qkv_geglu(M, ars_mode):
     C = 320
     h = (torch.randn(M, C) * 1.5 + 0.7).to(DEV, BF)
     hf = h.float()
-    rows = torch.stack([hf.sum(1), (hf * hf).sum(1)], 1).contiguous()
+    rows = torch.stack([hf.double().sum(1), (hf.double() ** 2).sum(1)], 1).contiguous()
     ln = torch.nn.LayerNorm(C)
     with torch.no_grad():
         ln.weight.uniform_(0.5, 1.5)

@@ -147,22 +147,25 @@ def test_linear_and_geglu(M, Kd, N, dt):
     assert rel_err(g, h * F.gelu(gate)) < tol(dt)
 
 
+@pytest.mark.parametrize("offset", [0.7, 60.0])
 @pytest.mark.parametrize("M,C", [(4096, 320), (1024, 640), (256, 1280), (333, 320)])
-def test_linear_layernorm_fold(M, C):
+def test_linear_layernorm_fold(M, C, offset):
     """norm -> Linear as ONE GEMM on the raw rows: the producer GEMM (with a residual) sums each
     stored row's (sum, sumsq) in its epilogue (row_stats), the consumer applies
     rstd (x W'^T - mean c1) + W beta + b in its epilogue (packed_ln_fold) — NHWC (QKV) and GEGLU
     (ff.net.0) outputs, against torch fp32 LayerNorm + Linear on the same bf16 rows."""
     torch.manual_seed(21)
+    # offset 60: rows whose mean is ~40x their spread (the fold's E[x^2] - mean^2 must not cancel:
+    # the row statistics and the variance are fp64)
     x = (torch.randn(M, C) * 1.5 + 0.7).to(DEV, torch.bfloat16)
-    res = torch.randn(M, C).to(DEV, torch.bfloat16)
+    res = (torch.randn(M, C) + offset).to(DEV, torch.bfloat16)
     prod = torch.nn.Linear(C, C)
     pp = K.PackedConv(prod.weight.to(DEV), prod.bias.to(DEV), torch.bfloat16)
-    rows = torch.zeros(M, 2, device=DEV)
+    rows = torch.zeros(M, 2, device=DEV, dtype=torch.float64)
     h = K.linear(pp, x, residual=res, row_stats=rows)
     hf = h.float()
-    assert torch.allclose(rows[:, 0], hf.sum(1), rtol=1e-4, atol=1e-2)
-    assert torch.allclose(rows[:, 1], (hf * hf).sum(1), rtol=1e-4, atol=1e-1)
+    assert torch.allclose(rows[:, 0], hf.double().sum(1), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(rows[:, 1], (hf.double() ** 2).sum(1), rtol=1e-4, atol=1e-1)
     ln = torch.nn.LayerNorm(C)
     with torch.no_grad():
         ln.weight.uniform_(0.5, 1.5)

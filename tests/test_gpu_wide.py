@@ -65,7 +65,7 @@ def test_wide_layernorm_fold_qkv_geglu(M, C, wide):
     torch.manual_seed(7)
     h = (torch.randn(M, C) * 1.5 + 0.7).to(DEV, BF)
     hf = h.float()
-    rows = torch.stack([hf.sum(1), (hf * hf).sum(1)], 1).contiguous()
+    rows = torch.stack([hf.double().sum(1), (hf.double() ** 2).sum(1)], 1).contiguous()
     ln = torch.nn.LayerNorm(C)
     with torch.no_grad():
         ln.weight.uniform_(0.5, 1.5)

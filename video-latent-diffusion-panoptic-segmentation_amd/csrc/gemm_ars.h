@@ -303,8 +303,8 @@ __global__ __launch_bounds__(256, 1) void gemm_ars_kernel(const ConvArgs p, int 
 #pragma unroll
           for (int o2 = 8; o2 > 0; o2 >>= 1) { a += __shfl_xor(a, o2, 64); b += __shfl_xor(b, o2, 64); }
           if (c16 == 0 && m < p.M) {
-            atomicAdd(p.row_stats + 2 * (int64_t)m, a);
-            atomicAdd(p.row_stats + 2 * (int64_t)m + 1, b);
+            unsafeAtomicAdd(p.row_stats + 2 * (int64_t)m, (double)a);
+            unsafeAtomicAdd(p.row_stats + 2 * (int64_t)m + 1, (double)b);
           }
         }
       }
@@ -552,8 +552,8 @@ __global__ __launch_bounds__(256, 2) void gemm_ars2_kernel(const ConvArgs p, int
 #pragma unroll
             for (int o2 = 8; o2 > 0; o2 >>= 1) { a += __shfl_xor(a, o2, 64); b += __shfl_xor(b, o2, 64); }
             if (c16 == 0 && m < p.M) {
-              atomicAdd(p.row_stats + 2 * (int64_t)m, a);
-              atomicAdd(p.row_stats + 2 * (int64_t)m + 1, b);
+              unsafeAtomicAdd(p.row_stats + 2 * (int64_t)m, (double)a);
+              unsafeAtomicAdd(p.row_stats + 2 * (int64_t)m + 1, (double)b);
             }
           }
         }
@@ -580,7 +580,7 @@ bool ars_legal(const ldm_conv_params* q, int es, bool mixed) {
   if (q->out_f32 || q->temb || q->gn_partial) return false;
   if (q->out_layout == LDM_OUT_GEGLU && (q->residual || q->row_stats || q->act != LDM_ACT_NONE)) return false;
   if (!a16(q->out) || !a16(q->residual) || !a16(q->bias) || !a16(q->ln_c1) || !a16(q->row_stats)) return false;
-  if (q->ln_rows && (reinterpret_cast<uintptr_t>(q->ln_rows) & 7)) return false;
+  if (q->ln_rows && (reinterpret_cast<uintptr_t>(q->ln_rows) & 15)) return false;
   return true;
 }
 // planner: 64x64-level shapes (>= 64 panels of 256 rows)

@@ -40,18 +40,41 @@ constexpr int NSLOT = 2;
 constexpr int SLOT_U4 = (BM + BN) * 8;      // uint4 per slot (72 KB)
 constexpr int A_INS = BM / 8 / 8;           // A DMA instructions per wave and K tile (8 rows each): 4
 constexpr int B_INS = BN / 8 / 8;           // 5
-// scratch floats per tile: bias [320] at 0, c1 [320] at 512, rows [256][2] at 1024 — six wave DMA
-// instructions of 256 floats, each from one source (the buffer descriptor is wave-uniform)
-constexpr int SCR_F = 1536;
+// scratch floats per tile: bias [320] at 0, c1 [320] at 512, fp64 rows [256][2] at 1024 — eight
+// wave DMA instructions of 1 KB (one per wave), each from one source (the buffer descriptor is
+// wave-uniform).  Issued with a tile's SECOND K tile (after every wave left the previous tile's
+// epilogue), so one buffer suffices.
+constexpr int SCR_F = 2048;
+// L2 prefetch: the 576 operand lines of K tile s + 2 are touched by 1-byte LDS-DMA loads (64 per
+// instruction, into a dummy LDS row per wave) while K tile s + 1 streams, so the DMA of every K tile
+// finds its lines in the XCD's L2 instead of waiting on Infinity-Cache / HBM latency
+constexpr int PF_INS = 2;                   // per wave: 72 of the 576 lines
+constexpr int PF_BYTES = 64 * 8;            // dummy LDS: 64 B per wave
 constexpr int SCR_C1 = 512, SCR_ROW = 1024;
 constexpr int NST = FM * FN / 2;            // epilogue store instructions per lane (20)
 }  // namespace wide
+
+// One byte per lane global -> LDS (M0 + lane): an L2 prefetch of the lane's line that needs no
+// destination VGPR (a register load would leave a late write the compiler does not know about).
+// Counted on vmcnt like the operand DMA.
+__device__ __forceinline__ void touch1(__amdgpu_buffer_rsrc_t rsrc, int voff, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_ubyte %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+      : "memory");
+}
 
 // GEGLU: the epilogue form (one instantiation per form)
 template <bool GEGLU>
 __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   using namespace wide;
-  __shared__ uint4 smem[NSLOT * SLOT_U4 + 2 * SCR_F / 4];
+  __shared__ uint4 smem[NSLOT * SLOT_U4 + SCR_F / 4 + PF_BYTES / 16];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -62,7 +85,7 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   // (lane & 7) ^ ((row >> 1) & 7) (source-side swizzle; (row >> 1) & 7 does not depend on i)
   const int drow = lane >> 3;
   const int dchunk = (lane & 7) ^ (((8 * wv + drow) >> 1) & 7);
-  const int scr_ins = wv < 6 ? 1 : 0;                               // scratch DMA (tile's first K tile)
+  // scratch DMA on a tile's first K tile: one instruction per wave
 
   const int tiles_m = (p.M + BM - 1) / BM;
   const int ntiles = tiles_m * p.tiles_n;
@@ -80,6 +103,7 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
   const unsigned scr0 = lds0 + NSLOT * SLOT_U4 * 16;
   float* scr = reinterpret_cast<float*>(smem + NSLOT * SLOT_U4);
+  const unsigned pf0 = scr0 + SCR_F * 4 + wv * 64;
   const __amdgpu_buffer_rsrc_t ra0 = __builtin_amdgcn_make_buffer_rsrc((void*)p.a0, 0, p.a0_bytes, kBufFlags);
   const __amdgpu_buffer_rsrc_t ra1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(p.a1 ? p.a1 : p.a0), 0, p.a1 ? p.a1_bytes : 0, kBufFlags);
@@ -89,7 +113,7 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   const __amdgpu_buffer_rsrc_t rc1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_c1, 0, p.ln_rows ? p.n * 4 : 0, kBufFlags);
   const __amdgpu_buffer_rsrc_t rrow =
-      __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_rows, 0, p.ln_rows ? p.M * 8 : 0, kBufFlags);
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.ln_rows, 0, p.ln_rows ? p.M * 16 : 0, kBufFlags);
   const int n_out = GEGLU ? (p.n >> 1) : p.n;
   const __amdgpu_buffer_rsrc_t rout =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.out, 0, (int)((int64_t)p.M * n_out * 2), kBufFlags);
@@ -130,17 +154,49 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
       const int off = n < p.n ? (n * p.kpad + k0 + dchunk * 8) * 2 : kOOB;
       dma16(rw, off, __builtin_amdgcn_readfirstlane(bbase + q * 8 * 128));
     }
-    if (kt == 0 && scr_ins) {
-      // instruction wv: 0, 1 bias [256 wv, +256); 2, 3 c1; 4, 5 rows [m0 + 128 (wv - 4), +128)
-      const unsigned sb = scr0 + (unsigned)((r & 1) * SCR_F * 4) + wv * 1024;
-      const int e = (wv & 1) * 256 + lane * 4;          // first float of this lane's 16 B
-      int off;
-      if (wv < 4) off = e < BN ? (n0 + e) * 4 : kOOB;
-      else off = (m0 * 2 + e) * 4;
+    if (kt == 1) {
+      // instruction wv: 0, 1 bias [256 wv, +256); 2, 3 c1; 4..7 fp64 rows [m0 + 64 (wv - 4), +64)
+      const unsigned sb = scr0 + wv * 1024;
+      const int e = (wv & 1) * 256 + lane * 4;          // first float of this lane's 16 B (bias / c1)
+      const int off = wv < 4 ? (e < BN ? (n0 + e) * 4 : kOOB) : (m0 * 16 + (wv - 4) * 1024 + lane * 16);
       const unsigned dst = __builtin_amdgcn_readfirstlane(sb);
       if (wv < 2) dma16(rbias, off, dst);
       else if (wv < 4) dma16(rc1, off, dst);
       else dma16(rrow, off, dst);
+    }
+  };
+
+  // touch (L2 prefetch) the operand lines of K tile s: line L = 72 wv + 64 i + lane < 72 (wv + 1);
+  // L < 256: A row m0 + L, else B row n0 + L - 256 (one 128-B line each)
+  auto prefetch = [&](int s) {
+#ifdef LDM_ABL_NO_PREFETCH
+    return;
+#endif
+    const int r = s / nks, kt = s - r * nks;
+    int m0, n0;
+    coords(r, m0, n0);
+    const int k0 = kt * KS;
+    const int sel = (p.c1 > 0 && k0 >= p.c0) ? 1 : 0;
+    const int cs = sel ? p.c1 : p.c0;
+    const int kk = sel ? k0 - p.c0 : k0;
+#pragma unroll
+    for (int i = 0; i < PF_INS; ++i) {
+      const int j = 64 * i + lane;
+      const int L = 72 * wv + j;
+      int off_a = kOOB, off_b = kOOB;
+      if (j < 72) {
+        if (L < BM) {
+          const int m = m0 + L;
+          if (m < p.M) off_a = (m * cs + kk) * 2;
+        } else {
+          const int n = n0 + L - BM;
+          if (n < p.n) off_b = (n * p.kpad + k0) * 2;
+        }
+      }
+      // the A and B lines of one instruction may both occur: two loads, each with the other's lanes
+      // out of range (no memory access)
+      touch1(sel ? ra1 : ra0, off_a, pf0);
+      touch1(rw, off_b, pf0);
     }
   };
 
@@ -179,6 +235,7 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   };
 
   if (total > 0) issue(0);
+  if (total > 1) prefetch(1);
   int s = 0;
   for (int r = 0; r < my_tiles; ++r) {
     int m0, n0;
@@ -188,27 +245,29 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     for (int kt = 0; kt < nks; ++kt, ++s) {
-      // K tile s landed for this wave; after an epilogue its NST stores (issued after the DMA) may
-      // stay in flight
-      if (kt == 0 && r > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+      // K tile s landed for this wave; younger and allowed to stay in flight: the prefetch of K tile
+      // s + 1 (issued right after this tile's DMA) and, after an epilogue, its NST stores
+      const bool pf = s + 1 < total, epi = kt == 0 && r > 0;
+      if (pf && epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PF_INS + NST) : "memory");
+      else if (epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+      else if (pf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PF_INS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // every wave's part of tile s is in LDS, and every wave is done with slot (s + 1) & 1
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (s + 1 < total) issue(s + 1);
+      if (s + 2 < total) prefetch(s + 2);
       compute(s & 1);
     }
-    // ---- epilogue from registers; this tile's scratch landed with its first slice
-    const float* sbias = scr + (r & 1) * SCR_F;
+    // ---- epilogue from registers; this tile's scratch landed with its second K tile
+    const float* sbias = scr;
     const float* sc1 = sbias + SCR_C1;
-    const float2* srow = reinterpret_cast<const float2*>(sbias + SCR_ROW);
+    const double2* srow = reinterpret_cast<const double2*>(sbias + SCR_ROW);
     float2 lnr[FM];
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
       if (p.ln_rows) {
-        const float2 st = srow[wm * WM + i * 16 + lr];
-        const float mean = st.x * p.ln_inv_k;
-        const float rstd = rsqrtf(fmaxf(st.y * p.ln_inv_k - mean * mean, 0.f) + p.ln_eps);
-        lnr[i] = make_float2(rstd, -rstd * mean);
+        const double2 st = srow[wm * WM + i * 16 + lr];
+        lnr[i] = ln_row_from(st.x, st.y, p.ln_inv_k, p.ln_eps);
       } else {
         lnr[i] = make_float2(1.f, 0.f);
       }
@@ -293,7 +352,7 @@ static int g_wide_mode = 0;   // tuning hook: 0 planner, 1 never, 2 whenever leg
 bool wide_legal(const ldm_conv_params* q, int es, bool mixed) {
   const auto a16 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; };
   if (es != 2 || mixed || q->ksize != 1 || q->stride != 1 || q->upsample || q->pad_mode != 0) return false;
-  // >= 2 K tiles per tile: a tile's scratch buffer is rewritten only after its epilogue
+  // >= 2 K tiles per tile: the scratch arrives with a tile's second K tile
   if (q->c0 % wide::KS || q->c1 % wide::KS || q->kpad % wide::KS || q->kpad < 2 * wide::KS || q->n % wide::BN)
     return false;
   if (q->out_layout != LDM_OUT_NHWC && q->out_layout != LDM_OUT_GEGLU) return false;
@@ -302,7 +361,7 @@ bool wide_legal(const ldm_conv_params* q, int es, bool mixed) {
   if (!a16(q->out) || !a16(q->bias) || !a16(q->ln_c1)) return false;
   if (q->ln_rows && (reinterpret_cast<uintptr_t>(q->ln_rows) & 15)) return false;
   const int64_t M = (int64_t)q->batch * q->h_out * q->w_out;
-  if (M * q->n * 2 >= (1LL << 31) - 64 || M * 8 >= (1LL << 31)) return false;
+  if (M * q->n * 2 >= (1LL << 31) - 64 || M * 16 >= (1LL << 31)) return false;
   return true;
 }
 

@@ -1228,7 +1228,7 @@ int validate(const ldm_conv_params* q, int* es_out) {
         !a16(q->residual) || !a16(q->bias) || q->n % 32)
       return LDM_ERR_ARG;
     if (q->row_stats && (q->out_layout != LDM_OUT_NHWC || !a16(q->row_stats))) return LDM_ERR_ARG;
-    if (q->ln_rows && (!q->ln_c1 || !a16(q->ln_c1) || (reinterpret_cast<uintptr_t>(q->ln_rows) & 7) ||
+    if (q->ln_rows && (!q->ln_c1 || !a16(q->ln_c1) || !a16(q->ln_rows) ||
                        q->ln_inv_k <= 0.f || (q->out_layout != LDM_OUT_NHWC && q->out_layout != LDM_OUT_GEGLU)))
       return LDM_ERR_ARG;
     if (!g_epi_pre && q->out_layout == LDM_OUT_NHWC) return LDM_ERR_ARG;

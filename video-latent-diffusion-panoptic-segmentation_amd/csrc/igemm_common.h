@@ -30,8 +30,8 @@ struct ConvArgs {
                       // per gn_unit-channel unit atomically, into slot (tile row index) % gn_slots)
   int gn_unit, gn_slots;
   int epi_pre;        // 1: the bf16 pre-activated staging epilogue where legal (A/B hook)
-  float* row_stats;   // optional [M][2] (sum, sumsq) of every stored output row (atomic adds)
-  const float* ln_rows;   // optional LayerNorm fold: [M][2] (sum, sumsq) of the A rows ...
+  double* row_stats;  // optional [M][2] fp64 (sum, sumsq) of every stored output row (atomic adds)
+  const double* ln_rows;  // optional LayerNorm fold: [M][2] fp64 (sum, sumsq) of the A rows ...
   const float* ln_c1;     // ... and [n] column sums of the gamma-scaled weight
   float ln_inv_k, ln_eps;
   int tap_inner;      // K tiles visited channel-block-major, taps inner (see k_state)
@@ -455,13 +455,17 @@ __device__ __forceinline__ uint4 pack8(const float* v) {
   return *reinterpret_cast<const uint4*>(h);
 }
 
-// LayerNorm fold: (rstd, -rstd * mean) of A row m from its (sum, sumsq)
+// LayerNorm fold: (rstd, -rstd * mean) of a row from its fp64 (sum, sumsq): the variance is taken
+// in fp64, so E[x^2] - mean^2 does not cancel for rows whose mean is large against their spread
+__device__ __forceinline__ float2 ln_row_from(double sum, double sumsq, float inv_k, float eps) {
+  const double mean = sum * (double)inv_k;
+  const double var = fmax(sumsq * (double)inv_k - mean * mean, 0.0);
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  return make_float2(rstd, (float)(-(double)rstd * mean));
+}
 __device__ __forceinline__ float2 ln_row(const ConvArgs& p, int m) {
-  const float2 st = *reinterpret_cast<const float2*>(p.ln_rows + 2 * (int64_t)m);
-  const float mean = st.x * p.ln_inv_k;
-  const float var = fmaxf(st.y * p.ln_inv_k - mean * mean, 0.f);
-  const float rstd = rsqrtf(var + p.ln_eps);
-  return make_float2(rstd, -rstd * mean);
+  const double2 st = *reinterpret_cast<const double2*>(p.ln_rows + 2 * (int64_t)m);
+  return ln_row_from(st.x, st.y, p.ln_inv_k, p.ln_eps);
 }
 
 // rows [m0, m0 + rows) cover at most two batches (the fast path holds two time embeddings)
@@ -643,8 +647,8 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
         a += red[(r * CW + c) * 2];
         b += red[(r * CW + c) * 2 + 1];
       }
-      atomicAdd(p.row_stats + 2 * (int64_t)(m0 + r), a);
-      atomicAdd(p.row_stats + 2 * (int64_t)(m0 + r) + 1, b);
+      unsafeAtomicAdd(p.row_stats + 2 * (int64_t)(m0 + r), (double)a);       // fp64: order-exact
+      unsafeAtomicAdd(p.row_stats + 2 * (int64_t)(m0 + r) + 1, (double)b);
     }
   }
   if (!stats) return;

@@ -533,8 +533,8 @@ class UNet(nn.Module):
         h = K.group_norm(x, B, N, t.groups, *p["norm"], 1e-6)
         cross = p["attn2"] is not None and ehs is not None
         if self.ln_fold and "qkv_ln" in p:
-            rs1 = K.zeroed_f32(2 * B * N, x.device)
-            rs3 = None if cross else K.zeroed_f32(2 * B * N, x.device)
+            rs1 = K.zeroed_f64(2 * B * N, x.device)
+            rs3 = None if cross else K.zeroed_f64(2 * B * N, x.device)
             h = K.linear(p["proj_in"], h, row_stats=rs1)                 # [B, N, C] + row (sum, sumsq)
             qkv = K.linear(p["qkv_ln"], h, ln=(rs1, p["ln_eps"][0]))      # = to_qkv(norm1(h))
         else:

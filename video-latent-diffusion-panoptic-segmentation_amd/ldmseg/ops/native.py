@@ -375,10 +375,10 @@ def gn_arena(key, device):
         _gn_arena_sizes[key] = max(need, st["used"])
 
 
-def zeroed_f32(count, device):
-    """A zeroed fp32 tensor of ``count`` (even) elements, from the enclosing gn_arena if any
+def zeroed_f64(count, device):
+    """A zeroed fp64 tensor of ``count`` (even) elements, from the enclosing gn_arena if any
     (LayerNorm row statistics share the GroupNorm accumulators' one memset)."""
-    return _gn_accumulators(1, 1, (count + 3) // 4, device).view(torch.float32).view(-1)[:count]
+    return _gn_accumulators(1, 1, (count + 1) // 2, device).view(-1)[:count]
 
 
 def _gn_accumulators(batch, slots, n, device):
@@ -405,7 +405,7 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
     into fp64 accumulators (from the enclosing gn_arena when there is one); they are attached to
     the returned tensor and consumed by group_norm().
 
-    row_stats: a zeroed fp32 [M, 2] tensor the epilogue adds each output row's (sum, sumsq) to.
+    row_stats: a zeroed fp64 [M, 2] tensor the epilogue adds each output row's (sum, sumsq) to.
     ln = (rows, eps): x0's rows are LayerNorm'd inside the GEMM (pc from packed_ln_fold, rows =
     the producer's row_stats)."""
     lib = load_library()
@@ -458,15 +458,15 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
         unit, slots = gn_unit_for(n), gn_slots_for(ho * wo)
         part = _gn_accumulators(batch, slots, n // unit, x0.device)
     ln_rows, ln_c1, ln_inv_k, ln_eps = None, None, 0.0, 0.0
-    if row_stats is not None and (row_stats.dtype != torch.float32 or row_stats.numel() != 2 * M
+    if row_stats is not None and (row_stats.dtype != torch.float64 or row_stats.numel() != 2 * M
                                   or not row_stats.is_contiguous()):
-        raise ValueError("row_stats must be a contiguous fp32 [M, 2] tensor")
+        raise ValueError("row_stats must be a contiguous fp64 [M, 2] tensor")
     if ln is not None:
         ln_rows, eps = ln
         if getattr(pc, "ln_c1", None) is None:
             raise ValueError("ln needs a packed_ln_fold weight")
-        if ln_rows.dtype != torch.float32 or ln_rows.numel() != 2 * M or not ln_rows.is_contiguous():
-            raise ValueError("ln rows must be a contiguous fp32 [M, 2] tensor")
+        if ln_rows.dtype != torch.float64 or ln_rows.numel() != 2 * M or not ln_rows.is_contiguous():
+            raise ValueError("ln rows must be a contiguous fp64 [M, 2] tensor")
         ln_c1, ln_inv_k, ln_eps = pc.ln_c1, 1.0 / (c0 + c1), float(eps)
     p = ConvParams(_ptr(x0), _ptr(x1), c0, c1, batch, h, w, ho, wo, pc.ksize, stride, int(upsample), _ptr(pc.w),
                    n, pc.kpad, _ptr(pc.bias), _ptr(temb), temb_stride, _ptr(residual), _ptr(out), out_layout, act,
