@@ -31,6 +31,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "UNet denoising steps/sec (T=8, 4×64×64 latent)"
 PEAK_BF16_TFLOPS = 2500.0     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_FP32_TFLOPS = 157.3      # fp32 MFMA = vector rate
+PEAK_FP8_TFLOPS = 5000.0      # dense fp8 MFMA (2x bf16; the headline figures with sparsity are not used)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -53,7 +54,17 @@ def make_scheduler(dev):
     return s
 
 
-def roofline(unet, stepper, ts, nsteps, dtype):
+def parse_latent(spec):
+    """'64' -> (64, 64); '32x64' -> (32, 64)."""
+    parts = str(spec).lower().split("x")
+    if len(parts) == 1:
+        return int(parts[0]), int(parts[0])
+    if len(parts) == 2:
+        return int(parts[0]), int(parts[1])
+    raise SystemExit(f"--latent: expected L or HxW, got {spec!r}")
+
+
+def roofline(unet, stepper, ts, nsteps, dtype, fp8=False):
     from ldmseg.ops import native as K
     prof = K.LaunchProfiler()
     K.set_profiler(prof)
@@ -80,8 +91,11 @@ def roofline(unet, stepper, ts, nsteps, dtype):
                  gflop=round(v["flops"] / nsteps / 1e9, 2), mb=round(v["bytes"] / nsteps / 1e6, 2))
         sec = v["ms"] * 1e-3
         if v["flops"] > 0:      # MFMA-bound family: fraction of the dense MFMA peak
+            pk = PEAK_FP8_TFLOPS if (fp8 and k == "attention") else peak_tf
             e["tflops"] = round(v["flops"] / sec / 1e12, 1)
-            e["frac_mfma"] = round(v["flops"] / sec / 1e12 / peak_tf, 4)
+            e["frac_mfma"] = round(v["flops"] / sec / 1e12 / pk, 4)
+            if pk != peak_tf:
+                e["peak_tflops"] = pk
         e["gbs"] = round(v["bytes"] / sec / 1e9, 1)
         e["frac_hbm"] = round(v["bytes"] / sec / 1e9 / PEAK_HBM_GBS, 4)
         per_step[k] = e
@@ -122,9 +136,9 @@ def pmc_traffic(family):
     return None, None
 
 
-def cpu_baseline(unet, budget_s=25.0):
+def cpu_baseline(unet, budget_s=25.0, frames=8, lh=64, lw=64):
     """Oracle restatement (oracle/unet.py + oracle/ddim.py, fp32 torch on the host cores),
-    bounded sample: whole frames of the T=8 step until ~budget_s, scaled to steps/s."""
+    bounded sample: whole frames of the T=`frames` step until ~budget_s, scaled to steps/s."""
     from oracle import ddim as oddim
     from oracle import unet as ounet
     host = host_cores()
@@ -134,21 +148,22 @@ def cpu_baseline(unet, budget_s=25.0):
     cfg = dict(unet.config)
     _, ac, final = oddim.tables("scaled_linear", 1000, 0.00085, 0.012, False)
     g = torch.Generator().manual_seed(5)
+    T = frames
     frames, elapsed = 0, 0.0
     with torch.no_grad():
-        while elapsed < budget_s and frames < 8:
-            x = torch.randn(1, 4, 64, 64, generator=g)
-            rgb = torch.randn(1, 4, 64, 64, generator=g)
+        while elapsed < budget_s and frames < T:
+            x = torch.randn(1, 4, lh, lw, generator=g)
+            rgb = torch.randn(1, 4, lh, lw, generator=g)
             t0 = time.perf_counter()
             eps = ounet.forward(sd, cfg, torch.cat([x, rgb], 1), torch.tensor(979))
             oddim.step(ac, final, 1000, 50, eps, 979, x)
             elapsed += time.perf_counter() - t0
             frames += 1
-    per_step = elapsed / frames * 8
+    per_step = elapsed / frames * T
     return {"value": round(1.0 / per_step, 5), "unit": "steps/s", "cores": threads, "kind": "port",
             "host": host,
-            "sample": f"{frames} frame(s) of one T=8 denoising step (UNet fwd + DDIM, fp32, 64x64), "
-                      f"{elapsed:.1f} s, scaled x{8 / frames:g} to one 8-frame step"}
+            "sample": f"{frames} frame(s) of one T={T} denoising step (UNet fwd + DDIM, fp32, {lh}x{lw}), "
+                      f"{elapsed:.1f} s, scaled x{T / frames:g} to one {T}-frame step"}
 
 
 def host_cores():
@@ -180,7 +195,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames", type=int, default=8, help="T: frames per clip (folded into the batch)")
-    ap.add_argument("--latent", type=int, default=64)
+    ap.add_argument("--latent", default="64", help="latent side L (LxL) or HxW, e.g. 32x64 for config 5's 256x512 frames")
+    ap.add_argument("--fp8", action="store_true",
+                    help="config 5: self-attention on the fp8 (e4m3) MFMA path (UNet.set_attention_fp8)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -212,12 +229,17 @@ def main():
 
     from ldmseg.pipelines import DenoiseStep
     unet = build_unet(dev, dtype)
+    if args.fp8:
+        if dtype != torch.bfloat16:
+            raise SystemExit("--fp8 needs --dtype bf16")
+        unet.set_attention_fp8(True)
     sched = make_scheduler(dev)
-    B, L = args.frames, args.latent
+    B = args.frames
+    LH, LW = parse_latent(args.latent)
     g = torch.Generator().manual_seed(1 + rank)                    # each rank: its own clip
-    rgb = torch.randn(B, 4, L, L, generator=g).to(dev)
+    rgb = torch.randn(B, 4, LH, LW, generator=g).to(dev)
     stepper = DenoiseStep(unet, sched, rgb, self_condition=False, use_graph=not args.no_graph)
-    stepper.set_latents(torch.randn(B, 4, L, L, generator=g).to(dev))
+    stepper.set_latents(torch.randn(B, 4, LH, LW, generator=g).to(dev))
     ts = [int(t) for t in sched.timesteps]
 
     for i in range(args.warmup):
@@ -239,21 +261,24 @@ def main():
     elapsed = sorted(windows)[len(windows) // 2]          # median window (median of 5)
     finite = bool(torch.isfinite(stepper.lat).all().item())
 
-    rl = roofline(unet, stepper, ts, args.profile_steps, dtype) if rank == 0 else None
+    rl = roofline(unet, stepper, ts, args.profile_steps, dtype, fp8=args.fp8) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(unet)
+        cpu = cpu_baseline(unet, frames=B, lh=LH, lw=LW)
     if rank == 0:
+        headline = (B, LH, LW) == (8, 64, 64) and not args.fp8
+        workload = f"UNet fwd (B={B} frames = one T={B} clip, 8x{LH}x{LW} input) + DDIM step, HIP graph per step"
+        if args.fp8:
+            workload += ", self-attention on the fp8 e4m3 MFMA (BASELINE config 5)"
         line = {
-            "metric": METRIC, "value": round(world * args.steps / elapsed, 4), "unit": "steps/s",
+            "metric": METRIC if headline else f"UNet denoising steps/sec (T={B}, 4x{LH}x{LW} latent)", "value": round(world * args.steps / elapsed, 4), "unit": "steps/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": args.dtype,
-            "data": "synthetic: random-init SD-1.4 UNet weights, N(0,1) KITTI-shaped 4x64x64 latents",
-            "config": {"workload": f"UNet fwd (B={B} frames = one T={B} clip, 8x{L}x{L} input) + DDIM step, "
-                                   "HIP graph per step",
+            "data": f"synthetic: random-init SD-1.4 UNet weights, N(0,1) KITTI-shaped 4x{LH}x{LW} latents",
+            "config": {"workload": workload,
                        "model": "SD-1.4 UNet2DConditionModel, cross-attn removed, 8-ch conv_in (815.5M)",
-                       "global_batch": B * world, "seq_len": L * L,
+                       "global_batch": B * world, "seq_len": LH * LW,
                        "parallelism": f"replicas x{world} (independent clips, no data-path collective)"},
             "outputs_finite": finite,
             "windows_ms_per_step": [round(w / args.steps * 1e3, 3) for w in windows],
@@ -291,7 +316,7 @@ def main_sample(args):
     vae_image = GeneralVAEImage().to(dev, dtype).eval()
     vae_seg = GeneralVAESeg(in_channels=16, int_channels=256, out_channels=128, block_out_channels=(32, 64, 128, 256),
                             num_upscalers=2, scaling_factor=0.2).to(dev, dtype).eval()
-    B, L = args.frames, args.latent
+    B, L = args.frames, parse_latent(args.latent)[0]
     steps = args.steps if args.steps != 20 else 3        # default: 3 timed clips
     warm = min(args.warmup, 1)
     g = torch.Generator().manual_seed(1 + rank)
@@ -437,7 +462,7 @@ def main_train(args):
     step = LDMTrainStep(u, sched, lr=1e-4, weight_decay=0.05, clip_grad=1.0, self_condition=True,
                         compute_dtype=torch.bfloat16 if args.dtype == "bf16" else torch.float32, seed=1 + rank,
                         zero_redundancy=args.zero)
-    B, L = args.clips * args.frames, args.latent
+    B, L = args.clips * args.frames, parse_latent(args.latent)[0]
     g = torch.Generator().manual_seed(100 + rank)
     lat = (torch.randn(B, 4, L, L, generator=g)).to(dev)
     rgb = (torch.randn(B, 4, L, L, generator=g)).to(dev)

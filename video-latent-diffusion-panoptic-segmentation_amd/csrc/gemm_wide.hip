@@ -370,8 +370,10 @@ int wide_bm(const ldm_conv_params* q, int es, bool mixed, int M, bool plan_force
   if (g_wide_mode == 1 || plan_forced || !wide_legal(q, es, mixed)) return 0;
   if (g_wide_mode == 2) return wide::BM;
   const int tiles = ((M + wide::BM - 1) / wide::BM) * (q->n / wide::BN);
-  // enough tiles to give every CU one, K deep enough to amortise the per-tile epilogue
-  if (tiles >= 256 && q->kpad >= 320) return wide::BM;
+  // enough tiles to give every CU one, K deep enough to amortise the per-tile epilogue: K = 320 (five
+  // K tiles) stays on the two-blocks-per-CU tiles / gemm_ars (r03a graph-step breakdown: QKV 320 ->
+  // 960 57 -> 73 us and the GEGLU 320 -> 2560 100 -> 106 us on this kernel)
+  if (tiles >= 256 && q->kpad >= 384) return wide::BM;
   return 0;
 }
 
