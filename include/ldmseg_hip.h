@@ -112,6 +112,11 @@ typedef struct {
 /* Deep-K / few-tile shapes are split over K into an fp32 slab; this returns its size (0: none). */
 size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* p);
 int ldm_conv2d(const ldm_conv_params* p, ldm_stream_t stream);
+/* The kernel and tile plan ldm_conv2d would run for p (host only, no launch): out[0] kind
+ * (0 tile kernel, 1 halo 3x3, 2 wide persistent 1x1, 3 A-register-stationary 1x1, 4 large
+ * 256x160 tile), out[1] bm, out[2] bn, out[3] ksplit, out[4] LDS stages.  LDM_OK or the
+ * validation error ldm_conv2d would return. */
+int ldm_conv2d_describe_plan(const ldm_conv_params* p, int* out);
 /* Tuning hook (benchmarks and tests only, not thread-safe): force the tile plan of every
  * following ldm_conv2d call where it is legal — bm in {32, 64, 128} x bn in {32, 64, 128},
  * or bm = 256 for the large-tile bf16 kernel (bn 160); ksplit >= 1 (clamped).  bm = 0
@@ -165,6 +170,9 @@ int ldm_attention_fp8(const ldm_attn_params* p, ldm_stream_t stream);
 /* Tuning hook (benchmarks / tests only): 1 routes bf16 through the 16x16x16-MFMA kernel
  * instead of the 16x16x32 one; 0 restores the default. */
 void ldm_attention_force_legacy(int legacy);
+/* Tuning / A-B hook: 1 (default) runs the bf16 backward for head_dim <= 64 on the 32x32x16 MFMA
+ * kernels, 0 on the 16x16x16 ones. */
+void ldm_attention_set_bwd32(int enabled);
 /* Tuning hook (A/B only), head_dim 40: 2 (default) the 32x32x16-MFMA kernel; 1 the 16x16x32 kernel
  * with the softmax scale and running max carried in the Q.K^T head-dim padding; 0 the 16x16x32
  * kernel with one FMA per score. */
@@ -437,24 +445,27 @@ int ldm_mse_loss(const void* pred, const float* target, const float* mask, const
 int ldm_sq_norm(const float* g, int64_t n, double* sum, int accumulate, void* workspace, ldm_stream_t stream);
 
 /* ldm_repack — refresh packed weights in place from their fp32 source parameters (the training
- * step, after each optimizer update), one launch over a device array of descriptors.  Chunk
- * index space: descriptor i covers chunks [chunk0_i, chunk0_{i+1}) (chunk0 ascending, starting
- * at 0), 8 destination elements per chunk.
+ * step, after each optimizer update), one launch over a device array of descriptors.  Tile index
+ * space: descriptor i covers tiles [chunk0_i, chunk0_{i+1}) (chunk0 ascending, starting at 0);
+ * modes 0 / 1 have ceil(rows / 16) * ceil(cpad / 64) tiles (16 destination rows x 64 channels,
+ * every tap), mode 2 ceil(rows / 2048).
  *   mode 0: forward pack, bf16 dst[row0 + r][kpad], r < rows: dst[..][(ky*ks + kx)*cpad + c] =
  *           W[r'][c][ky][kx] (W fp32 [co][ci][ks][ks]; r' = r, or the GEGLU 16-interleave's source
  *           row when geglu; zero where r' >= co, c >= ci or the tap is past ks*ks)
  *   mode 1: data-gradient pack (ldmseg packed_dgrad): dst[row0 + r][(ky*ks + kx)*cpad + c] =
  *           W[c'][r][ks-1-ky][ks-1-kx], r < rows = ci, c' = c or its GEGLU source row, c < co
  *   mode 2: fp32 vector dst[row0 + j] = src[j'] for j < rows (j' = j or its GEGLU source row,
- *           co = the vector length).  rows = elements, chunks = ceil(rows / 8).
- * f32: modes 0 / 1 write fp32 packs (the exact-fp32 compute path) instead of bf16. */
+ *           co = the vector length).  rows = elements.
+ * ks <= 3; cpad a multiple of 8.  f32: modes 0 / 1 write fp32 packs (the exact-fp32 compute path)
+ * instead of bf16.  Replaces the torch re-pack of every trainable weight after
+ * trainers_ldm_cond.py:769-781's optimizer step. */
 typedef struct {
   const float* src;
   void* dst;
   int64_t chunk0;
   int rows, row0, kpad, co, ci, ks, cpad, mode, geglu, f32;
 } ldm_repack_desc;
-int ldm_repack(const ldm_repack_desc* descs, int ndesc, int64_t total_chunks, ldm_stream_t stream);
+int ldm_repack(const ldm_repack_desc* descs, int ndesc, int64_t total_tiles, ldm_stream_t stream);
 
 /* Workspace of ldm_mse_loss / ldm_sq_norm: per-block fp64 partials, summed in a fixed order by a
  * second one-block pass (deterministic; no atomics). */

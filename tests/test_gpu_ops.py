@@ -283,7 +283,11 @@ def test_attention_softmax_spike_bf16(C, N, maxcol):
 # ------------------------------------------------------------------------------ norms
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("B,HW,c0,c1,G,eps,act", [(2, 4096, 320, 0, 32, 1e-5, True), (2, 256, 1280, 1280, 32, 1e-5, True),
-                                                  (3, 100, 640, 320, 32, 1e-6, False), (1, 64, 64, 0, 16, 1e-6, True)])
+                                                  (3, 100, 640, 320, 32, 1e-6, False), (1, 64, 64, 0, 16, 1e-6, True),
+                                                  # single-block small-image kernel (gn_small): config 5's 4x8 level,
+                                                  # an in-place concat, 10-channel groups straddling 16-B vectors
+                                                  (16, 32, 1280, 0, 32, 1e-5, True), (4, 32, 640, 640, 32, 1e-5, True),
+                                                  (2, 8, 320, 0, 32, 1e-6, False)])
 def test_group_norm(B, HW, c0, c1, G, eps, act, dt):
     torch.manual_seed(5)
     x = torch.randn(B, HW, c0 + c1) * 3 + 1.5

@@ -167,7 +167,8 @@ def test_layer_norm_grads(C, dt):
 
 
 # ------------------------------------------------------------------ attention
-@pytest.mark.parametrize("B,N,heads,d", [(2, 256, 8, 40), (1, 200, 8, 80), (2, 64, 8, 160), (1, 97, 2, 64)])
+@pytest.mark.parametrize("B,N,heads,d", [(2, 256, 8, 40), (1, 200, 8, 80), (2, 64, 8, 160), (1, 97, 2, 64),
+                                         (1, 300, 4, 32), (1, 4096, 8, 40), (1, 130, 2, 48)])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 def test_attention_grads(B, N, heads, d, dt):
     torch.manual_seed(5)
@@ -189,6 +190,30 @@ def test_attention_grads(B, N, heads, d, dt):
                     3 * C, 3 * C, dqkv, dqkv[..., C:], dqkv[..., 2 * C:], 3 * C, 3 * C)
     for i in range(3):
         assert rel(dqkv[..., i * C:(i + 1) * C], qr.grad[..., i * C:(i + 1) * C]) < tol(dt) * 4, i
+
+
+@pytest.mark.parametrize("N,d", [(4096, 40), (1000, 64), (77, 32)])
+def test_attention_bwd32_matches_16x16_kernels(N, d):
+    """The 32x32x16-MFMA backward (head_dim <= 64) against the 16x16x16 kernels it replaced, same
+    bf16 inputs: both are fp32-accumulated flash-attention backwards of the same P = 2^(S c2 - lse)."""
+    torch.manual_seed(9)
+    B, heads = 2, 8
+    C = heads * d
+    qq = (torch.randn(B, N, 3 * C, device=DEV) * 0.5).to(torch.bfloat16)
+    go = torch.randn(B, N, C, device=DEV).to(torch.bfloat16)
+    oo, lse = K.attention_fwd_lse(qq, qq[..., C:], qq[..., 2 * C:], B, heads, d, N, N, 3 * C, 3 * C, 3 * C)
+    outs = []
+    for new in (True, False):
+        K.set_attention_bwd32(new)
+        try:
+            dqkv = torch.empty_like(qq)
+            K.attention_bwd(qq, qq[..., C:], qq[..., 2 * C:], oo, go, lse, B, heads, d, N, N, 3 * C, 3 * C, 3 * C,
+                            dqkv, dqkv[..., C:], dqkv[..., 2 * C:], 3 * C, 3 * C)
+            outs.append(dqkv.float())
+        finally:
+            K.set_attention_bwd32(True)
+    for i in range(3):
+        assert rel(outs[0][..., i * C:(i + 1) * C], outs[1][..., i * C:(i + 1) * C]) < 1e-2, i
 
 
 # ------------------------------------------------------------------ loss / optimizer

@@ -1,0 +1,60 @@
+"""ldm_conv2d's planner on the host (ldm_conv2d_describe_plan; no GPU, nothing launches).
+
+The plans of the headline workload (BASELINE config: B = 8 frames at 64x64 latents) are pinned —
+they are the ones the bench and its rocprof profiles measure — and config 2's single frame must
+fill the chip: at B = 1 every 3x3 conv and deep-K GEMM is split into >= 128 blocks instead of the
+32 halo tiles / 64-160 blocks the B = 8 rules gave (profiles/r03g_b1_plans.txt).
+"""
+import pytest
+
+from ldmseg.ops import native as K
+
+
+def _p(**kw):
+    return K.describe_plan(**kw)
+
+
+def test_headline_plans_pinned():
+    # 3x3 at the 64x64 and 32x32 levels: halo-tiled, one block per CU
+    for hw, c in ((64, 320), (32, 640)):
+        pl = _p(batch=8, h=hw, w=hw, c0=c, n=c, temb=True, gn_stats=True)
+        assert pl["kind"] == "halo" and pl["blocks"] == 256, pl
+    # the [640 || 320] -> 320 up-block conv reads the concat in place on the halo kernel
+    assert _p(batch=8, h=64, w=64, c0=640, c1=320, n=320, residual=True, gn_stats=True)["kind"] == "halo"
+    # GEGLU: A-register-stationary at K = 320, the wide persistent tile at K = 640 / 1280
+    assert _p(batch=8 * 4096, h=1, w=1, c0=320, n=2560, ksize=1, ln=True, out_layout=K.OUT_GEGLU)["kind"] == "ars"
+    for hw, c in ((32, 640), (16, 1280)):
+        pl = _p(batch=8 * hw * hw, h=1, w=1, c0=c, n=8 * c, ksize=1, ln=True, out_layout=K.OUT_GEGLU)
+        assert pl["kind"] == "wide", pl
+    # QKV at K = 320 stays on the two-blocks-per-CU tiles (the wide tile lost there, r03a)
+    pl = _p(batch=8 * 4096, h=1, w=1, c0=320, n=960, ksize=1, ln=True, geglu_bias=False)
+    assert (pl["kind"], pl["bm"], pl["bn"]) == ("tile", 128, 160), pl
+    # deep K over few tiles: split to 512 blocks
+    pl = _p(batch=8, h=16, w=16, c0=1280, n=1280, temb=True, gn_stats=True)
+    assert (pl["bm"], pl["bn"], pl["ksplit"], pl["blocks"]) == (128, 160, 4, 512), pl
+    pl = _p(batch=8, h=8, w=8, c0=1280, n=1280, temb=True, gn_stats=True)
+    assert (pl["bm"], pl["bn"], pl["ksplit"], pl["blocks"]) == (64, 160, 8, 512), pl
+    pl = _p(batch=8, h=8, w=8, c0=1280, c1=1280, n=1280, residual=True, gn_stats=True)
+    assert (pl["bm"], pl["bn"], pl["ksplit"]) == (128, 160, 16), pl
+
+
+@pytest.mark.parametrize("hw,c0,c1,n", [(64, 320, 0, 320), (64, 640, 320, 320), (32, 320, 0, 640), (32, 640, 0, 640),
+                                        (32, 1280, 640, 640), (16, 640, 0, 1280), (16, 1280, 0, 1280),
+                                        (16, 2560, 0, 1280), (8, 1280, 0, 1280), (8, 1280, 1280, 1280)])
+def test_single_frame_convs_fill_the_chip(hw, c0, c1, n):
+    pl = _p(batch=1, h=hw, w=hw, c0=c0, c1=c1, n=n, residual=True, gn_stats=True)
+    assert pl["kind"] == "tile" and pl["blocks"] >= 128, pl
+    if hw >= 16:
+        assert pl["blocks"] >= 256, pl
+
+
+@pytest.mark.parametrize("M,kin,n", [(1024, 2560, 640), (256, 5120, 1280), (64, 5120, 1280)])
+def test_single_frame_deep_gemms_split(M, kin, n):
+    pl = _p(batch=M, h=1, w=1, c0=kin, n=n, ksize=1, residual=True)
+    assert pl["ksplit"] > 1 and pl["blocks"] >= 128, pl
+
+
+def test_describe_plan_rejects_what_conv2d_rejects():
+    assert _p(batch=1, h=8, w=8, c0=12, n=64)["kind"] == "tile"     # c0 padded to 16: legal
+    with pytest.raises(RuntimeError):
+        _p(batch=1, h=8, w=8, c0=16, n=64, ksize=3, stride=2, upsample=True)   # upsample + stride 2

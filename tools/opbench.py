@@ -19,10 +19,12 @@ from ldmseg.ops import native as K  # noqa: E402
 
 DEV = "cuda"
 BF = torch.bfloat16
+BATCH = 8          # --batch: the conv / GEMM cases' B (their shapes are written for the bench's B = 8)
 
 
 def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, geglu=False, residual=False,
               temb=False, stats=False, c1=0):
+    B = max(1, B * BATCH // 8)
     g = torch.Generator(device=DEV).manual_seed(0)
     x0 = torch.randn(B, H, W, Cin - c1, device=DEV, generator=g).to(BF)
     x1 = torch.randn(B, H, W, c1, device=DEV, generator=g).to(BF) if c1 else None
@@ -56,6 +58,33 @@ def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2):
         K.set_attention_maxcol(maxcol)
         return K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, C // heads, N, N, 3 * C, 3 * C, 3 * C)
     return run, 4.0 * B * heads * N * N * (C // heads), None
+
+
+def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False):
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(B, H, W, Cin, device=DEV, generator=g).to(BF)
+    dy = torch.randn(B, H, W, Cout, device=DEV, generator=g).to(BF)
+    w = torch.randn(Cout, Cin, k, k, device=DEV, generator=g) * 0.05
+    pc = K.PackedConv(w, None, BF, geglu=geglu)
+    dw = torch.empty(Cout, Cin, k, k, device=DEV) if k == 3 else torch.empty(Cout, Cin, device=DEV)
+
+    def run():
+        return K.conv2d_wgrad(pc, x, B, H, W, dy, dw=dw)
+    return run, 2.0 * B * H * W * Cout * k * k * Cin, None
+
+
+def attn_bwd_case(B, N, C, heads=8, new=True):
+    d = C // heads
+    qkv = (torch.randn(B, N, 3 * C, device=DEV) * 0.5).to(BF)
+    go = torch.randn(B, N, C, device=DEV).to(BF)
+    o, lse = K.attention_fwd_lse(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, d, N, N, 3 * C, 3 * C, 3 * C)
+    dqkv = torch.empty_like(qkv)
+
+    def run():
+        K.set_attention_bwd32(new)
+        return K.attention_bwd(qkv, qkv[..., C:], qkv[..., 2 * C:], o, go, lse, B, heads, d, N, N, 3 * C, 3 * C,
+                               3 * C, dqkv, dqkv[..., C:], dqkv[..., 2 * C:], 3 * C, 3 * C)
+    return run, 10.0 * B * heads * N * N * d, None     # five N x N x d matmuls (S, dP, dV, dK, dQ)
 
 
 def gn_case(B, HW, C, stats):
@@ -151,6 +180,18 @@ CASES = {
     "attn_1024_d80_w8": lambda: attn_case(8, 1024, 640, waves=8),
     "attn_4096_d40_w4": lambda: attn_case(8, 4096, 320, waves=4),
     "attn_256_d160": lambda: attn_case(8, 256, 1280),
+    "wgrad_l0_320": lambda: wgrad_case(16, 64, 64, 320, 320),
+    "wgrad_l1_640": lambda: wgrad_case(16, 32, 32, 640, 640),
+    "wgrad_l2_1280": lambda: wgrad_case(16, 16, 16, 1280, 1280),
+    "wgrad_l3_1280": lambda: wgrad_case(16, 8, 8, 1280, 1280),
+    "wgrad_up_960": lambda: wgrad_case(16, 64, 64, 960, 320),
+    "wgrad_geglu_320": lambda: wgrad_case(16, 64, 64, 320, 2560, k=1, geglu=True),
+    "wgrad_ff2_1280": lambda: wgrad_case(16, 64, 64, 1280, 320, k=1),
+    "wgrad_proj_320": lambda: wgrad_case(16, 64, 64, 320, 320, k=1),
+    "wgrad_qkv_320": lambda: wgrad_case(16, 64, 64, 320, 960, k=1),
+    "attn_bwd_4096_d40": lambda: attn_bwd_case(16, 4096, 320),
+    "attn_bwd_4096_d40_old": lambda: attn_bwd_case(16, 4096, 320, new=False),
+    "attn_bwd_1024_d80": lambda: attn_bwd_case(16, 1024, 640),
     "gn_l0_fused": lambda: gn_case(8, 4096, 320, True),
     "gn_l0_unfused": lambda: gn_case(8, 4096, 320, False),
     "gn_l1_fused": lambda: gn_case(8, 1024, 640, True),
@@ -180,14 +221,17 @@ def main():
                     help="wide-tile persistent 1x1 GEMM modes (ldm_conv2d_set_wide: 0 planner, 1 never, 2 BM 256, 3 BM 128)")
     ap.add_argument("--skcols", nargs="*", type=int, default=[0],
                     help="split-K reduction tile widths to compare (ldm_conv2d_set_splitk_cols: 0 planner, 64, 128)")
+    ap.add_argument("--batch", type=int, default=8, help="B of the conv / GEMM cases (config 2: 1)")
     a = ap.parse_args()
+    global BATCH
+    BATCH = a.batch
     if a.lib:
         K.load_library(os.path.abspath(a.lib))
     K.set_conv_epilogue(a.epi)
     names = a.only or list(CASES)
     built = {}
     for n in names:
-        if not n.startswith(("conv", "gemm")):
+        if not n.startswith(("conv", "gemm")) or n.startswith("wgrad"):
             built[n] = CASES[n]()
             continue
         for pl in a.plans:

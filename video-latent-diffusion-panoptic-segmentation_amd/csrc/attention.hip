@@ -1244,6 +1244,328 @@ __global__ __launch_bounds__(256, (sizeof(T) == 2 && DP <= 80) ? 2 : 1) void att
   }
 }
 
+// --------------------------------------------------------------------------------------
+// bf16 backward on the full-rate 32x32x16 MFMA (head_dim <= 32 NDB; the 16x16x16 kernels above
+// issue at half the FLOP rate on gfx950).  Layouts (32x32x16): A lane l = row l&31, k 8(l>>5)+j;
+// B lane l = col l&31, k 8(l>>5)+j; C lane l col l&31, reg r row (r&3) + 8(r>>2) + 4(l>>5).
+//   attn_bwd_kv32: a wave owns 32 keys (K, V rows as B operands in registers), loops over
+//     64-query tiles of (Q, dO) staged by LDS-DMA (plus the tile's lse and D in LDS):
+//       S = Q K^T, dP = dO V^T          (A = Q / dO rows; acc col = key, rows = queries)
+//       P = 2^(S c2 - lse), dZ = P (dP - D)
+//       dV^T += dO^T P, dK^T += Q^T dZ  (A = dO^T / Q^T by ds_read_b64_tr_b16 in the permuted
+//                                        k order of the acc registers, B = the bf16 acc: as the
+//                                        forward's P.V, attn_d40_kernel)
+//   attn_bwd_q32: a wave owns 32 queries (Q, dO rows as B operands), loops over 64-key tiles of
+//     (K, V):  S^T = K Q^T, dP^T = V dO^T, dZ^T = P^T (dP^T - D), dQ^T += K^T dZ^T.
+// Per 64-row tile and wave: 28 (kv) / 20 (q) MFMAs of 32 cycles against 48 / 32 half-rate 16x16x16
+// issues of 16 keys (or queries) per wave before.
+// --------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+template <int NDB>
+struct Bwd32 {
+  static constexpr int CPR = NDB * 4;          // 16-byte chunks staged per row: NDB * 32 columns
+  static constexpr int RCH = CPR + 1;          // + one pad chunk
+  static constexpr int ROW = RCH * 8;          // bf16 elements per LDS row
+  static constexpr int TILE = 64 * ROW;        // elements per staged operand tile
+};
+
+// rows [r0, r0 + 64) of two bf16 [n][stride] operands (head h) -> LDS tiles [64][ROW], zero past
+// n and head_dim; RCH wave instructions of 1 KB each per operand
+template <int NDB, int NW>
+__device__ __forceinline__ void stage_pair32(const bf16_t* ap, int as, const bf16_t* bp, int bs, int n, int dh,
+                                             int r0, unsigned abase, unsigned bbase, int wave, int lane) {
+  constexpr int RCH = Bwd32<NDB>::RCH, CPR = Bwd32<NDB>::CPR;
+  for (int i = wave; i < RCH; i += NW) {
+    const int L = i * 64 + lane;
+    const int row = L / RCH, c = L - row * RCH;
+    const int r = r0 + row, dd = c * 8;
+    const bool ok = r < n && c < CPR && dd < dh;
+    const unsigned off = __builtin_amdgcn_readfirstlane(i * 64 * 16);
+    glds16(ok ? (const void*)(ap + (int64_t)r * as + dd) : (const void*)&kZeros16, abase + off);
+    glds16(ok ? (const void*)(bp + (int64_t)r * bs + dd) : (const void*)&kZeros16, bbase + off);
+  }
+}
+
+// A operand X^T (rows d = 32 db + l&31, k = reduction rows of block blk, k-step st, in the acc's
+// permuted order 16 st + 8 (j >> 2) + 4 hh + (j & 3)) from a row-major [64][ROW] tile
+template <int ROW>
+__device__ __forceinline__ bf16x8_t tr_a32(const bf16_t* tile, int blk, int st, int db, int lane) {
+  typedef __attribute__((ext_vector_type(4))) short s4_t;
+  typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+  const int i16 = lane & 15, hh = lane >> 5;
+  const int cb = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+  const bf16_t* a0 = tile + (32 * blk + 16 * st + 4 * hh + (i16 >> 2)) * ROW + cb;
+  const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0)));
+  const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0 + 8 * ROW)));
+  return __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+}
+
+__device__ __forceinline__ bf16x8_t pack8_bf16(const float* v) {
+  return __builtin_bit_cast(bf16x8_t, make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                                 pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7])));
+}
+
+__device__ __forceinline__ f32x16_t mma32(const bf16x8_t a, const bf16x8_t b, f32x16_t c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int NC, int NDB>
+__global__ __launch_bounds__(256, 2) void attn_bwd_kv32(const AttnBwdArgs p) {
+  using G = Bwd32<NDB>;
+  constexpr int ROW = G::ROW, TILE = G::TILE;
+  __shared__ uint4 smem[(2 * 2 * TILE * 2 + 2 * 128 * 4) / 16];
+  bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
+  float* const vec = reinterpret_cast<float*>(lds + 2 * 2 * TILE);     // [buf][lse 64 | D 64]
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int key = blockIdx.x * 128 + wave * 32 + r32;
+  const bf16_t* qp = reinterpret_cast<const bf16_t*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
+  const bf16_t* dop = reinterpret_cast<const bf16_t*>(p.dout) + (int64_t)b * p.nq * p.dos + (int64_t)h * p.d;
+  const bf16_t* kp = reinterpret_cast<const bf16_t*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
+  const bf16_t* vp = reinterpret_cast<const bf16_t*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * p.d;
+  const float* lse = p.lse + ((int64_t)b * p.heads + h) * p.nq;
+  const float* dvec = p.dvec + ((int64_t)b * p.heads + h) * p.nq;
+
+  bf16x8_t kf[NC], vf[NC];                 // B operands: K / V row of this lane's key, d 16c + 8hh ..
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int dd = 16 * c + 8 * hh;
+    uint4 kk = make_uint4(0u, 0u, 0u, 0u), vv = kk;
+    if (key < p.nkv && dd < p.d) {
+      kk = *reinterpret_cast<const uint4*>(kp + (int64_t)key * p.ks + dd);
+      vv = *reinterpret_cast<const uint4*>(vp + (int64_t)key * p.vs + dd);
+    }
+    kf[c] = __builtin_bit_cast(bf16x8_t, kk);
+    vf[c] = __builtin_bit_cast(bf16x8_t, vv);
+  }
+  f32x16_t dkt[NDB], dvt[NDB];
+#pragma unroll
+  for (int i = 0; i < NDB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { dkt[i][r] = 0.f; dvt[i][r] = 0.f; }
+  const float c2 = p.scale_log2;
+
+  auto stage = [&](int q0, int buf) {
+    const unsigned qb = lds0 + (unsigned)(buf * 2 * TILE * 2);
+    stage_pair32<NDB, 4>(qp, p.qs, dop, p.dos, p.nq, p.d, q0, qb, qb + TILE * 2, wave, lane);
+  };
+  // the tile's lse (+inf past nq: P = 0 there) and D, register-staged by the first two waves
+  auto vec_load = [&](int q0) -> float {
+    const int q = q0 + (tid & 63);
+    if (tid < 64) return q < p.nq ? lse[q] : INFINITY;
+    if (tid < 128) return q < p.nq ? dvec[q] : 0.f;
+    return 0.f;
+  };
+  auto vec_store = [&](int buf, float v) {
+    if (tid < 128) vec[buf * 128 + tid] = v;
+  };
+
+  auto compute = [&](int buf) {
+    const bf16_t* Qs = lds + buf * 2 * TILE;
+    const bf16_t* Ds = Qs + TILE;
+    const float* lv = vec + buf * 128;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      f32x16_t s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const uint4 qa = *reinterpret_cast<const uint4*>(Qs + (32 * qb + r32) * ROW + 16 * c + 8 * hh);
+        const uint4 da = *reinterpret_cast<const uint4*>(Ds + (32 * qb + r32) * ROW + 16 * c + 8 * hh);
+        s = mma32(__builtin_bit_cast(bf16x8_t, qa), kf[c], s);
+        dp = mma32(__builtin_bit_cast(bf16x8_t, da), vf[c], dp);
+      }
+      // rows: query 32 qb + (r & 3) + 8 (r >> 2) + 4 hh
+      bf16x8_t pb[2], zb[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        float pv[8], zv[8];
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+          const int g4 = 2 * st + jj;
+          const float4 l4 = *reinterpret_cast<const float4*>(lv + 32 * qb + 8 * g4 + 4 * hh);
+          const float4 d4 = *reinterpret_cast<const float4*>(lv + 64 + 32 * qb + 8 * g4 + 4 * hh);
+          const float lq[4] = {l4.x, l4.y, l4.z, l4.w}, dq[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = 4 * g4 + e;
+            const float pr = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lq[e]));
+            pv[4 * jj + e] = pr;
+            zv[4 * jj + e] = pr * (dp[r] - dq[e]);
+          }
+        }
+        pb[st] = pack8_bf16(pv);
+        zb[st] = pack8_bf16(zv);
+      }
+#pragma unroll
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          dvt[db] = mma32(tr_a32<ROW>(Ds, qb, st, db, lane), pb[st], dvt[db]);   // dV^T += dO^T P
+          dkt[db] = mma32(tr_a32<ROW>(Qs, qb, st, db, lane), zb[st], dkt[db]);   // dK^T += Q^T dZ
+        }
+    }
+  };
+
+  const int ntiles = (p.nq + 63) / 64;
+  stage(0, 0);
+  vec_store(0, vec_load(0));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    float nv = 0.f;
+    if (t + 1 < ntiles) {
+      stage((t + 1) * 64, buf ^ 1);
+      nv = vec_load((t + 1) * 64);
+    }
+    compute(buf);
+    if (t + 1 < ntiles) vec_store(buf ^ 1, nv);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (key >= p.nkv) return;
+  bf16_t* dkp = reinterpret_cast<bf16_t*>(p.dk) + ((int64_t)b * p.nkv + key) * p.dkvs + (int64_t)h * p.d;
+  bf16_t* dvp = reinterpret_cast<bf16_t*>(p.dv) + ((int64_t)b * p.nkv + key) * p.dkvs + (int64_t)h * p.d;
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 32 * db + 8 * g4 + 4 * hh;
+      if (d0 >= p.d) continue;
+      const int r = 4 * g4;
+      *reinterpret_cast<uint2*>(dkp + d0) =
+          make_uint2(pack_bf16x2(dkt[db][r] * p.scale, dkt[db][r + 1] * p.scale),
+                     pack_bf16x2(dkt[db][r + 2] * p.scale, dkt[db][r + 3] * p.scale));
+      *reinterpret_cast<uint2*>(dvp + d0) =
+          make_uint2(pack_bf16x2(dvt[db][r], dvt[db][r + 1]), pack_bf16x2(dvt[db][r + 2], dvt[db][r + 3]));
+    }
+}
+
+template <int NC, int NDB>
+__global__ __launch_bounds__(256, 2) void attn_bwd_q32(const AttnBwdArgs p) {
+  using G = Bwd32<NDB>;
+  constexpr int ROW = G::ROW, TILE = G::TILE;
+  __shared__ uint4 smem[2 * 2 * TILE * 2 / 16];
+  bf16_t* const lds = reinterpret_cast<bf16_t*>(smem);
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5;
+  const int h = blockIdx.y, b = blockIdx.z;
+  const int qi = blockIdx.x * 128 + wave * 32 + r32;
+  const bf16_t* qp = reinterpret_cast<const bf16_t*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
+  const bf16_t* dop = reinterpret_cast<const bf16_t*>(p.dout) + (int64_t)b * p.nq * p.dos + (int64_t)h * p.d;
+  const bf16_t* kp = reinterpret_cast<const bf16_t*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
+  const bf16_t* vp = reinterpret_cast<const bf16_t*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * p.d;
+  const bool qok = qi < p.nq;
+  const float lse_q = qok ? p.lse[((int64_t)b * p.heads + h) * p.nq + qi] : 0.f;
+  const float d_q = qok ? p.dvec[((int64_t)b * p.heads + h) * p.nq + qi] : 0.f;
+
+  bf16x8_t qf[NC], gf[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int dd = 16 * c + 8 * hh;
+    uint4 qq = make_uint4(0u, 0u, 0u, 0u), gg = qq;
+    if (qok && dd < p.d) {
+      qq = *reinterpret_cast<const uint4*>(qp + (int64_t)qi * p.qs + dd);
+      gg = *reinterpret_cast<const uint4*>(dop + (int64_t)qi * p.dos + dd);
+    }
+    qf[c] = __builtin_bit_cast(bf16x8_t, qq);
+    gf[c] = __builtin_bit_cast(bf16x8_t, gg);
+  }
+  f32x16_t dqt[NDB];
+#pragma unroll
+  for (int i = 0; i < NDB; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dqt[i][r] = 0.f;
+  const float c2 = p.scale_log2;
+
+  auto stage = [&](int k0, int buf) {
+    const unsigned kb = lds0 + (unsigned)(buf * 2 * TILE * 2);
+    stage_pair32<NDB, 4>(kp, p.ks, vp, p.vs, p.nkv, p.d, k0, kb, kb + TILE * 2, wave, lane);
+  };
+  auto compute = [&](int buf, int k0, bool masked) {
+    const bf16_t* Ks = lds + buf * 2 * TILE;
+    const bf16_t* Vs = Ks + TILE;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      f32x16_t s, dp;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s[r] = 0.f; dp[r] = 0.f; }
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const uint4 ka = *reinterpret_cast<const uint4*>(Ks + (32 * kb + r32) * ROW + 16 * c + 8 * hh);
+        const uint4 va = *reinterpret_cast<const uint4*>(Vs + (32 * kb + r32) * ROW + 16 * c + 8 * hh);
+        s = mma32(__builtin_bit_cast(bf16x8_t, ka), qf[c], s);
+        dp = mma32(__builtin_bit_cast(bf16x8_t, va), gf[c], dp);
+      }
+      // rows: key 32 kb + (r & 3) + 8 (r >> 2) + 4 hh; column: this lane's query
+      bf16x8_t zb[2];
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        float zv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int r = 8 * st + j;
+          const float pr = __builtin_amdgcn_exp2f(fmaf(s[r], c2, -lse_q));
+          float z = pr * (dp[r] - d_q);
+          if (masked && k0 + 32 * kb + (r & 3) + 8 * (r >> 2) + 4 * hh >= p.nkv) z = 0.f;
+          zv[j] = z;
+        }
+        zb[st] = pack8_bf16(zv);
+      }
+#pragma unroll
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int st = 0; st < 2; ++st) dqt[db] = mma32(tr_a32<ROW>(Ks, kb, st, db, lane), zb[st], dqt[db]);
+    }
+  };
+
+  const int ntiles = (p.nkv + 63) / 64;
+  const int nfull = p.nkv / 64;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < ntiles) stage((t + 1) * 64, buf ^ 1);
+    if (t < nfull) compute(buf, t * 64, false);
+    else compute(buf, t * 64, true);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  if (!qok) return;
+  bf16_t* dqp = reinterpret_cast<bf16_t*>(p.dq) + ((int64_t)b * p.nq + qi) * p.dqs + (int64_t)h * p.d;
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d0 = 32 * db + 8 * g4 + 4 * hh;
+      if (d0 >= p.d) continue;
+      const int r = 4 * g4;
+      *reinterpret_cast<uint2*>(dqp + d0) =
+          make_uint2(pack_bf16x2(dqt[db][r] * p.scale, dqt[db][r + 1] * p.scale),
+                     pack_bf16x2(dqt[db][r + 2] * p.scale, dqt[db][r + 3] * p.scale));
+    }
+}
+
+int g_attn_bwd32 = 1;   // tuning / A-B hook (ldm_attention_set_bwd32): 0 routes bf16 to the 16x16x16 kernels
+
+template <int NC, int NDB>
+int launch_bwd32(const AttnBwdArgs& a, int batch, hipStream_t s) {
+  hipLaunchKernelGGL((attn_bwd_kv32<NC, NDB>), dim3((a.nkv + 127) / 128, a.heads, batch), dim3(256), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  hipLaunchKernelGGL((attn_bwd_q32<NC, NDB>), dim3((a.nq + 127) / 128, a.heads, batch), dim3(256), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
 template <typename T, int DP>
 int launch_bwd_dp(const AttnBwdArgs& a, int batch, hipStream_t s) {
   hipLaunchKernelGGL((attn_bwd_kv<T, DP>), dim3((a.nkv + 63) / 64, a.heads, batch), dim3(256), 0, s, a);
@@ -1259,6 +1581,15 @@ int launch_bwd(const AttnBwdArgs& a, int batch, hipStream_t s) {
   hipLaunchKernelGGL(attn_bwd_dot<T>, dim3((rows + 15) / 16), dim3(256), 0, s, a, batch);
   LDM_CHECK_LAUNCH();
   const int dp = (a.d + 15) / 16 * 16;
+  if constexpr (sizeof(T) == 2) {
+    // 32x32x16 forms: 16-byte-aligned row strides (the B-operand rows are 16-byte register loads)
+    const bool al = a.qs % 8 == 0 && a.dos % 8 == 0 && a.ks % 8 == 0 && a.vs % 8 == 0;
+    if (g_attn_bwd32 && al && a.d <= 64) {
+      if (a.d <= 32) return launch_bwd32<2, 1>(a, batch, s);
+      if (a.d <= 48) return launch_bwd32<3, 2>(a, batch, s);
+      return launch_bwd32<4, 2>(a, batch, s);
+    }
+  }
   switch (dp) {
     case 16: return launch_bwd_dp<T, 16>(a, batch, s);
     case 32: return launch_bwd_dp<T, 32>(a, batch, s);
@@ -1321,6 +1652,7 @@ extern "C" int ldm_attention_fp8(const ldm_attn_params* q, ldm_stream_t stream) 
 extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 || waves == 8) ? waves : 0; }
 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
+extern "C" void ldm_attention_set_bwd32(int enabled) { g_attn_bwd32 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_maxcol(int mode) {
   g_attn_maxcol = mode >= 1 ? 1 : 0;     // 0: per-score FMA, 16x16x32 kernel
   g_attn_d40 = mode >= 2 ? 1 : 0;        // 1: max column, 16x16x32 kernel; 2: 32x32x16 d = 40 kernel

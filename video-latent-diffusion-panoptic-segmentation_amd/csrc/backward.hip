@@ -121,6 +121,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
   const int hin_v = p.upsample ? 2 * p.h_in : p.h_in, win_v = p.upsample ? 2 * p.w_in : p.w_in;
 
   auto issue = [&](int mb, int buf) {
+#ifdef LDM_ABL_NO_LOADS
+    return;
+#endif
     const unsigned dyb = lds0 + (unsigned)(buf * 2 * WG_IMG);
     const unsigned xb = dyb + WG_IMG;
 #pragma unroll
@@ -162,6 +165,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
       for (int i = 0; i < NF; ++i) af[i] = wg_frag<T>(dyi, 32 * s, wn * WT + 16 * i, lane);
 #pragma unroll
       for (int j = 0; j < NF; ++j) bf[j] = wg_frag<T>(xi, 32 * s, wk * WT + 16 * j, lane);
+#ifdef LDM_ABL_NO_MFMA
+      if constexpr (sizeof(T) == 2) {
+#pragma unroll
+        for (int i = 0; i < NF; ++i) asm volatile("" ::"v"(af[i].v.x), "v"(bf[i].v.x));
+        continue;
+      }
+#endif
 #pragma unroll
       for (int i = 0; i < NF; ++i)
 #pragma unroll

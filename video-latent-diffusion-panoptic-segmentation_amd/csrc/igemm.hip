@@ -1071,10 +1071,28 @@ Plan make_plan_base(const ldm_conv_params* q, int M, int es, bool mixed_src);
 // GEGLU on 128x128 (the register epilogue needs a wave N extent of 32k)
 Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
   Plan pl = make_plan_base(q, M, es, mixed_src);
+  // few tiles (config 2's B = 1; the B = 8 plans all give >= 512 blocks): 64x160 tiles split K toward
+  // ~512 blocks (profiles/r03g_b1_plans.txt, eager us: 3x3 320 at 64x64 69.7 -> 32.4, 3x3 640 at
+  // 32x32 78.2 -> 31.2, the [640 || 320] -> 320 up-block conv 166.7 -> 49.6, FF2 2560 27.5 -> 20.5)
+  if (!g_force_bm && es == 2 && !mixed_src && q->out_layout != LDM_OUT_GEGLU && q->out_layout != LDM_OUT_SHUFFLE2) {
+    const int nk = q->kpad / (128 / es);
+    const int tn = (q->n + 159) / 160;
+    const int t64 = ((M + 63) / 64) * tn;
+    const int tiles_now = ((M + pl.bm - 1) / pl.bm) * ((q->n + pl.bn - 1) / pl.bn) * pl.ksplit;
+    if (tn * 160 * 10 <= q->n * 11 && nk >= 32 && tiles_now < 384 && t64 < 384) {
+      const int ks = std::max(1, std::min(std::min(16, nk / 4), (512 + t64 / 2) / t64));
+      if (t64 * ks >= tiles_now) { pl.bm = 64; pl.bn = 160; pl.ksplit = ks; pl.stages = 2; }
+    }
+  }
   if (q->row_stats || q->ln_rows) {
     pl.ksplit = 1;
     pl.stages = 2;
-    if (q->out_layout == LDM_OUT_GEGLU) { pl.bm = 128; pl.bn = 128; }
+    if (q->out_layout == LDM_OUT_GEGLU) {
+      // 64x64 (wave N extent 32) when 128x128 tiles give < 512 blocks (B = 1: GEGLU 1280 at 16x16
+      // 26.9 -> 21.3 us)
+      const int t128 = ((M + 127) / 128) * ((q->n + 127) / 128);
+      pl.bm = pl.bn = t128 < 512 ? 64 : 128;
+    }
     else if (pl.bm == 256 || pl.bm < 64) { pl.bm = 128; pl.bn = 160; }
   }
   return pl;
@@ -1115,6 +1133,8 @@ Plan make_plan_base(const ldm_conv_params* q, int M, int es, bool mixed_src) {
     pl.bm = M <= 32 ? 32 : (M <= 64 ? 64 : 128);
     pl.bn = 128;
     if (tiles_of(pl.bm, 128) < 256) pl.bn = 64;
+    // few rows (B = 1): 64-row tiles (the 16x16-level GEGLU 1280 -> 10240 at B = 1: 25.9 -> 21.3 us)
+    if (pl.bm == 128 && tiles_of(128, pl.bn) < 512) pl.bm = 64;
     return pl;
   }
   // 128x160 / 64x160 (two blocks per CU, one block's epilogue under the other's MFMAs) beat the
@@ -1255,7 +1275,10 @@ bool is_mixed(const ldm_conv_params* q, int es) {
 bool use_halo_plan(const ldm_conv_params* q, int es, bool mixed) {
   if (g_halo_mode == 1 || mixed || g_force_bm || !halo_legal(q, es)) return false;
   if (g_halo_mode == 2) return true;
-  return q->n % halo::BN == 0 && (q->w_out == 64 || (q->w_out == 32 && q->c0 + q->c1 <= 960));
+  // >= 256 blocks (one per CU): at B = 1 the 4-row halo tiles give 32 (3x3 320 at 64x64: 69.7 us vs
+  // 32.4 on split 64x160 tiles)
+  const int64_t blocks = (int64_t)q->batch * q->h_out / 4 * (q->n / halo::BN);
+  return q->n % halo::BN == 0 && blocks >= 256 && (q->w_out == 64 || (q->w_out == 32 && q->c0 + q->c1 <= 960));
 }
 
 #include "gemm_ars.h"
@@ -1290,6 +1313,33 @@ extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   if (use_halo_plan(q, es, mixed) || ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0) || use_ars(q, es, mixed, M)) return 0;
   const Plan pl = make_plan(q, M, es, mixed);
   return pl.ksplit > 1 ? (size_t)pl.ksplit * M * q->n * sizeof(float) : 0;
+}
+
+extern "C" int ldm_conv2d_describe_plan(const ldm_conv_params* q, int* out) {
+  int es = 0;
+  const int st = validate(q, &es);
+  if (st != LDM_OK) return st;
+  if (!out) return LDM_ERR_ARG;
+  const int M = q->batch * q->h_out * q->w_out;
+  const bool mixed = is_mixed(q, es);
+  const bool halo = use_halo_plan(q, es, mixed);
+  const int wbm = halo ? 0 : ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0);
+  const bool ars = !halo && !wbm && use_ars(q, es, mixed, M);
+  if (halo || wbm || ars) {
+    out[0] = halo ? 1 : (wbm ? 2 : 3);
+    out[1] = halo ? q->w_out * 4 : wbm;
+    out[2] = halo ? halo::BN : (wbm ? 320 : 0);
+    out[3] = 1;
+    out[4] = 0;
+    return LDM_OK;
+  }
+  const Plan pl = make_plan(q, M, es, mixed);
+  out[0] = pl.bm == 256 ? 4 : 0;
+  out[1] = pl.bm;
+  out[2] = pl.bn;
+  out[3] = pl.ksplit;
+  out[4] = g_force_stages ? g_force_stages : pl.stages;
+  return LDM_OK;
 }
 
 extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {

@@ -397,8 +397,16 @@ __device__ __forceinline__ int geglu_src_row(int p, int half) {   // packed (int
   return w < 16 ? blk * 16 + w : half + blk * 16 + (w - 16);
 }
 
+// One block per tile of one descriptor (tile0 = the descriptor's first block): a tile is 16
+// destination rows x 64 channels over every tap.  The tile's source floats are read as contiguous
+// runs into LDS (a run per source row: 64 channels x taps, or 16 rows x taps), then written as
+// 16-byte rows of 8 consecutive destination elements — both the fp32 reads and the packed writes
+// are coalesced (the earlier element-per-chunk gather read the data-gradient packs' sources at a
+// stride of ci * 9 floats: 9.4 ms of a 142 ms training iteration, profiles/r03a_train_*).
+constexpr int RP_R = 16, RP_C = 64, RP_MAXT = 9, RP_VEC = 2048;
 __global__ __launch_bounds__(256) void repack_kernel(const ldm_repack_desc* __restrict__ d, int nd, int64_t total) {
-  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  __shared__ float lds[RP_R * RP_C * RP_MAXT];
+  const int64_t q = blockIdx.x;
   if (q >= total) return;
   int lo = 0, hi = nd - 1;
   while (lo < hi) {
@@ -408,57 +416,75 @@ __global__ __launch_bounds__(256) void repack_kernel(const ldm_repack_desc* __re
   const ldm_repack_desc e = d[lo];
   const int64_t local = q - e.chunk0;
   const float* src = e.src;
+  const int tid = threadIdx.x;
   if (e.mode == 2) {                                   // fp32 vector [row0 + j] = src[perm j]
     float* dst = static_cast<float*>(e.dst);
-    for (int k = 0; k < 8; ++k) {
-      const int j = (int)(local * 8) + k;
-      if (j >= e.rows) break;
+    for (int j = (int)local * RP_VEC + tid; j < e.rows && j < ((int)local + 1) * RP_VEC; j += 256)
       dst[e.row0 + j] = src[e.geglu ? geglu_src_row(j, e.co >> 1) : j];
-    }
     return;
   }
-  const int cpk = e.kpad >> 3;                         // 8-element chunks per packed row
-  const int r = (int)(local / cpk);
-  const int k0 = (int)(local - (int64_t)r * cpk) * 8;
-  const int taps = e.ks * e.ks;
-  float v8[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int kk = k0 + k;
-    const int tap = kk / e.cpad, c = kk - tap * e.cpad;
+  const int T = e.ks * e.ks;
+  const int nct = (e.cpad + RP_C - 1) / RP_C;
+  const int r0 = (int)(local / nct) * RP_R, c0 = (int)(local % nct) * RP_C;
+  const bool fwd = e.mode == 0;
+  // LDS image: fwd  lds[i][jj * T + t] = W[row'(r0 + i)][c0 + jj][t]        (run 64 T per source row)
+  //            dgrad lds[jj][i * T + t] = W[c'(c0 + jj)][r0 + i][t]          (run 16 T per source row)
+  const int nsrc = fwd ? RP_R : RP_C, run = fwd ? RP_C * T : RP_R * T;
+  for (int idx = tid; idx < nsrc * run; idx += 256) {
+    const int sr = idx / run, x = idx - sr * run;
     float v = 0.f;
-    if (tap < taps) {
-      const int ky = tap / e.ks, kx = tap - ky * e.ks;
-      if (e.mode == 0) {                               // W[co][ci][ky][kx] -> [co][(ky, kx, ci)]
-        const int co = e.geglu ? geglu_src_row(r, e.co >> 1) : r;
-        if (co < e.co && c < e.ci) v = src[(((int64_t)co * e.ci + c) * e.ks + ky) * e.ks + kx];
-      } else {                                         // W[co][ci][2-ky][2-kx] -> [ci][(ky, kx, co)]
-        const int co = e.geglu ? geglu_src_row(c, e.co >> 1) : c;
-        if (c < e.co && r < e.ci)
-          v = src[(((int64_t)co * e.ci + r) * e.ks + (e.ks - 1 - ky)) * e.ks + (e.ks - 1 - kx)];
-      }
+    if (fwd) {
+      const int r = r0 + sr;
+      const int co = e.geglu ? geglu_src_row(r, e.co >> 1) : r;
+      if (r < e.rows && co < e.co && c0 * T + x < e.ci * T)
+        v = src[((int64_t)co * e.ci + c0) * T + x];
+    } else {
+      const int c = c0 + sr;
+      const int co = e.geglu ? geglu_src_row(c, e.co >> 1) : c;
+      if (c < e.co && r0 * T + x < e.ci * T) v = src[((int64_t)co * e.ci + r0) * T + x];
     }
-    v8[k] = v;
+    lds[idx] = v;
   }
-  if (e.f32) {                                         // fp32 packs (the exact-fp32 compute path)
-    float* dst = static_cast<float*>(e.dst) + (int64_t)(e.row0 + r) * e.kpad + k0;
-    reinterpret_cast<float4*>(dst)[0] = make_float4(v8[0], v8[1], v8[2], v8[3]);
-    reinterpret_cast<float4*>(dst)[1] = make_float4(v8[4], v8[5], v8[6], v8[7]);
-    return;
-  }
-  bf16_t h[8];
+  __syncthreads();
+  // writes: item (i, tap, g) = destination row r0 + i, columns tap * cpad + c0 + 8 g .. + 7
+  for (int w = tid; w < RP_R * T * (RP_C / 8); w += 256) {
+    const int i = w / (T * 8), rem = w - i * (T * 8), tap = rem >> 3, g = rem & 7;
+    const int row = r0 + i, c = c0 + 8 * g;
+    if (row >= e.rows || c >= e.cpad) continue;
+    float v8[8];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) h[k] = f2bf(v8[k]);
-  bf16_t* dst = static_cast<bf16_t*>(e.dst);
-  *reinterpret_cast<uint4*>(dst + (int64_t)(e.row0 + r) * e.kpad + k0) = *reinterpret_cast<const uint4*>(h);
+    for (int k = 0; k < 8; ++k)
+      v8[k] = fwd ? lds[i * run + (8 * g + k) * T + tap] : lds[(8 * g + k) * run + i * T + (T - 1 - tap)];
+    const int64_t o = (int64_t)(e.row0 + row) * e.kpad + tap * e.cpad + c;
+    if (e.f32) {
+      float* dst = static_cast<float*>(e.dst) + o;
+      reinterpret_cast<float4*>(dst)[0] = make_float4(v8[0], v8[1], v8[2], v8[3]);
+      reinterpret_cast<float4*>(dst)[1] = make_float4(v8[4], v8[5], v8[6], v8[7]);
+    } else {
+      bf16_t h[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h[k] = f2bf(v8[k]);
+      *reinterpret_cast<uint4*>(static_cast<bf16_t*>(e.dst) + o) = *reinterpret_cast<const uint4*>(h);
+    }
+  }
+  // the K padding past the last tap (kpad > T * cpad) stays zero: rewritten by the first column tile
+  if (c0 == 0 && e.kpad > T * e.cpad) {
+    const int pad = e.kpad - T * e.cpad;
+    for (int w = tid; w < RP_R * pad; w += 256) {
+      const int i = w / pad, k = T * e.cpad + (w - i * pad);
+      if (r0 + i >= e.rows) continue;
+      const int64_t o = (int64_t)(e.row0 + r0 + i) * e.kpad + k;
+      if (e.f32) static_cast<float*>(e.dst)[o] = 0.f;
+      else static_cast<bf16_t*>(e.dst)[o] = f2bf(0.f);
+    }
+  }
 }
 }  // namespace
 
-extern "C" int ldm_repack(const ldm_repack_desc* descs, int ndesc, int64_t total_chunks, ldm_stream_t stream) {
-  if (!descs || ndesc <= 0 || total_chunks <= 0) return LDM_ERR_ARG;
+extern "C" int ldm_repack(const ldm_repack_desc* descs, int ndesc, int64_t total_tiles, ldm_stream_t stream) {
+  if (!descs || ndesc <= 0 || total_tiles <= 0 || total_tiles >= (1LL << 31)) return LDM_ERR_ARG;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(repack_kernel, dim3((unsigned)((total_chunks + 255) / 256)), dim3(256), 0, s, descs, ndesc,
-                     total_chunks);
+  hipLaunchKernelGGL(repack_kernel, dim3((unsigned)total_tiles), dim3(256), 0, s, descs, ndesc, total_tiles);
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }

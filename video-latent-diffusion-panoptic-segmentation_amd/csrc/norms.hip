@@ -185,6 +185,82 @@ __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x0, const 
   }
 }
 
+// Small images without producer statistics (config 5's 4x8 level: hw = 32, C = 1280, where a 64-row
+// conv tile spans two images so the producer cannot sum per-image units): one 512-thread block per
+// image stages the whole [hw][C] slab in LDS (<= GNS_MAX_BYTES) and takes EXACT two-pass group
+// statistics from it in a fixed order (per-channel partials of row phases, then per group), then
+// writes y — one launch instead of memset + statistics + apply (33 -> ~5 us per launch).
+constexpr int GNS_MAX_BYTES = 96 * 1024;
+template <typename T>
+__global__ __launch_bounds__(512) void gn_small(const T* __restrict__ x0, const T* __restrict__ x1, int c0, int c1,
+                                                int hw, int groups, float eps, const float* __restrict__ gamma,
+                                                const float* __restrict__ beta, int act, T* __restrict__ out,
+                                                float2* __restrict__ save) {
+  constexpr int EPC = 16 / sizeof(T);
+  extern __shared__ uint4 img[];                       // [hw][V] vectors, then [nph][C] fp32 partials
+  __shared__ float2 gst[64];
+  const int C = c0 + c1, V = C / EPC, cpg = C / groups;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int nph = 512 / V;                             // row phases of the per-channel partials
+  float* part = reinterpret_cast<float*>(img + (int64_t)hw * V);
+  for (int e = tid; e < hw * V; e += 512) {
+    const int r = e / V, v = e - r * V, c = v * EPC;
+    img[e] = c < c0 ? *reinterpret_cast<const uint4*>(x0 + ((int64_t)b * hw + r) * c0 + c)
+                    : *reinterpret_cast<const uint4*>(x1 + ((int64_t)b * hw + r) * c1 + (c - c0));
+  }
+  __syncthreads();
+  const int v = tid % V, ph = tid / V;
+  for (int pass = 0; pass < 2; ++pass) {               // 0: sums -> mean; 1: centred squares -> var
+    if (ph < nph) {
+      float acc[EPC], mu[EPC];
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) {
+        acc[k] = 0.f;
+        mu[k] = pass ? gst[(v * EPC + k) / cpg].x : 0.f;
+      }
+      for (int r = ph; r < hw; r += nph) {
+        const uint4 raw = img[r * V + v];
+        const T* e = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+        for (int k = 0; k < EPC; ++k) {
+          const float f = to_f(e[k]) - mu[k];
+          acc[k] += pass ? f * f : f;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) part[ph * C + v * EPC + k] = acc[k];
+    }
+    __syncthreads();
+    if (tid < groups) {
+      float a = 0.f;
+      for (int q = 0; q < nph; ++q)
+        for (int c = tid * cpg; c < (tid + 1) * cpg; ++c) a += part[q * C + c];
+      const float n = (float)hw * cpg;
+      if (pass == 0) gst[tid].x = a / n;
+      else gst[tid].y = 1.0f / sqrtf(a / n + eps);
+    }
+    __syncthreads();
+  }
+  if (save && tid < groups) save[b * groups + tid] = gst[tid];
+  for (int e = tid; e < hw * V; e += 512) {
+    const int r = e / V, vv = e - r * V;
+    const uint4 raw = img[e];
+    const T* x = reinterpret_cast<const T*>(&raw);
+    uint4 res;
+    T* o = reinterpret_cast<T*>(&res);
+#pragma unroll
+    for (int k = 0; k < EPC; ++k) {
+      const int c = vv * EPC + k;
+      const float2 ms = gst[c / cpg];
+      const float sc = ms.y * gamma[c];
+      float y = to_f(x[k]) * sc + (beta[c] - ms.x * sc);
+      if (act == LDM_ACT_SILU) y = silu_f(y);
+      o[k] = from_f<T>(y);
+    }
+    *reinterpret_cast<uint4*>(out + ((int64_t)b * hw + r) * C + vv * EPC) = res;
+  }
+}
+
 // LayerNorm over the last dim, two-pass (mean, then centred variance) in fp32 registers.
 // G lanes per row (G | 64): a wave normalises 64/G rows at once, each lane holding NV 16-byte
 // chunks (chunk v = lane_in_row + G * i), so C = 320 bf16 (40 chunks) runs 8 rows per wave
@@ -298,6 +374,21 @@ int gn_launch(const void* x0, const void* x1, int c0, int c1, int batch, int hw,
   constexpr int EPC = 16 / sizeof(T);
   const int C = c0 + c1, V = C / EPC;
   if ((a0 && !a1 && c1 > 0) || (!a0 && a1)) a0 = a1 = nullptr;     // one layout for both: recompute both
+  const size_t small_lds = (size_t)hw * C * sizeof(T) + (size_t)(512 / std::max(1, V)) * C * sizeof(float);
+  if (!a0 && V <= 512 && (size_t)hw * C * sizeof(T) <= GNS_MAX_BYTES && small_lds <= 128 * 1024) {
+    static bool attr_set = false;                    // > 64 KB of dynamic LDS: raise the kernel's cap once
+    if (!attr_set) {
+      if (hipFuncSetAttribute(reinterpret_cast<const void*>(&gn_small<T>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              128 * 1024) != hipSuccess)
+        return LDM_ERR_LAUNCH;
+      attr_set = true;
+    }
+    hipLaunchKernelGGL((gn_small<T>), dim3(batch), dim3(512), small_lds, s, static_cast<const T*>(x0),
+                       static_cast<const T*>(x1), c0, c1, hw, groups, eps, gamma, beta, act, static_cast<T*>(out),
+                       reinterpret_cast<float2*>(save));
+    LDM_CHECK_LAUNCH();
+    return LDM_OK;
+  }
   if (!a0) {
     unit = 1;
     slots = std::max(1, std::min(GN_STATS_SLOTS, GN_MAXC / C));    // slots x C entries fit the LDS

@@ -56,11 +56,14 @@ class PackRefresher:
     def _descs(self, P, D):
         recs = []
 
-        def add(src, dst, nchunks, rows, row0, kpad, co, ci, ks, cpad, mode, geglu):
+        def add(src, dst, rows, row0, kpad, co, ci, ks, cpad, mode, geglu):
             f32 = int(dst.dtype == torch.float32 and mode != 2)
             if dst.dtype not in (torch.float32, torch.bfloat16):
                 raise TypeError(f"ldm_repack writes bf16 / fp32 packs, not {dst.dtype}")
-            recs.append((src.data_ptr(), dst.data_ptr(), nchunks, rows, row0, kpad, co, ci, ks, cpad, mode, geglu,
+            if mode != 2 and (ks > 3 or cpad % 8):
+                raise ValueError("ldm_repack packs ks <= 3 with 8-aligned channel padding")
+            ntiles = -(-rows // 2048) if mode == 2 else -(-rows // 16) * -(-cpad // 64)
+            recs.append((src.data_ptr(), dst.data_ptr(), ntiles, rows, row0, kpad, co, ci, ks, cpad, mode, geglu,
                          f32))
 
         for pc in _iter_packs(P):
@@ -75,13 +78,13 @@ class PackRefresher:
                 co, ci = w.shape[0], w.shape[1]
                 ks = w.shape[2] if w.ndim == 4 else 1
                 rows = pc.n if len(ws) == 1 else co         # a single source may be row-padded (conv_out_t)
-                add(w, pc.w, rows * pc.kpad // 8, rows, row0, pc.kpad, co, ci, ks, pc.cin, 0, int(pc.geglu))
+                add(w, pc.w, rows, row0, pc.kpad, co, ci, ks, pc.cin, 0, int(pc.geglu))
                 row0 += rows
             bs = pc.src_b
             if pc.bias is not None and bs and not (len(bs) == 1 and pc.bias.data_ptr() == bs[0].data_ptr()):
                 j0 = 0
                 for b in bs:                                # concatenated / interleaved copy: refresh it
-                    add(b, pc.bias, (b.numel() + 7) // 8, b.numel(), j0, 0, b.numel(), 0, 1, 1, 2, int(pc.geglu))
+                    add(b, pc.bias, b.numel(), j0, 0, b.numel(), 0, 1, 1, 2, int(pc.geglu))
                     j0 += b.numel()
         for pc in _iter_packs(D):
             src = getattr(pc, "dg_src", None)
@@ -98,7 +101,7 @@ class PackRefresher:
             co = sum(w.shape[0] for w in ws)
             ci = w0.shape[1]
             ks = w0.shape[2] if w0.ndim == 4 else 1
-            add(w0, pc.w, pc.n * pc.kpad // 8, pc.n, 0, pc.kpad, co, ci, ks, pc.cin, 1, int(geglu))
+            add(w0, pc.w, pc.n, 0, pc.kpad, co, ci, ks, pc.cin, 1, int(geglu))
         return recs
 
     def _build(self):
@@ -106,9 +109,9 @@ class PackRefresher:
         self.fallback = []
         recs = self._descs(P, D or {})
         blob, c0 = bytearray(), 0
-        for (src, dst, nch, rows, row0, kpad, co, ci, ks, cpad, mode, geglu, f32) in recs:
+        for (src, dst, ntiles, rows, row0, kpad, co, ci, ks, cpad, mode, geglu, f32) in recs:
             blob += _DESC.pack(src, dst, c0, rows, row0, kpad, co, ci, ks, cpad, mode, geglu, f32)
-            c0 += nch
+            c0 += ntiles
         self.ndesc, self.total = len(recs), c0
         dev = self.u.device
         self.table = torch.frombuffer(blob, dtype=torch.uint8).to(dev) if recs else None

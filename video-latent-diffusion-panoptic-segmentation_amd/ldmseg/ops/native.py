@@ -62,6 +62,7 @@ EXPORTS = {
     "ldm_conv2d": (_i, [ctypes.POINTER(ConvParams), _vp]),
     "ldm_conv2d_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(ConvParams)]),
     "ldm_conv2d_force_plan": (None, [_i, _i, _i]),
+    "ldm_conv2d_describe_plan": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ctypes.c_int)]),
     "ldm_conv2d_force_stages": (None, [_i]),
     "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_conv2d_set_halo": (None, [_i]),
@@ -86,6 +87,7 @@ EXPORTS = {
     "ldm_gaussian_posterior": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
     "ldm_attention_fwd_lse": (_i, [ctypes.POINTER(AttnParams), _vp, _vp]),
     "ldm_attention_force_legacy": (None, [_i]),
+    "ldm_attention_set_bwd32": (None, [_i]),
     "ldm_attention_set_waves": (None, [_i]),
     "ldm_attention_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_bwd": (_i, [ctypes.POINTER(AttnParams), _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
@@ -129,9 +131,13 @@ _lib = None
 _lock = threading.Lock()
 
 
-def load_library(path=LIB_PATH):
-    """Load the HIP library (no GPU needed to load it; kernels need one to run)."""
+def load_library(path=None):
+    """Load the HIP library (no GPU needed to load it; kernels need one to run).  The env variable
+    LDMSEG_HIP_LIB selects another build of it (A/B runs of an ablation or older build, whose
+    tuning hooks may be missing: only those are then skipped)."""
     global _lib
+    override = path is not None or bool(os.environ.get("LDMSEG_HIP_LIB"))
+    path = path or os.environ.get("LDMSEG_HIP_LIB") or LIB_PATH
     with _lock:
         if _lib is None:
             if not os.path.exists(path):
@@ -140,6 +146,8 @@ def load_library(path=LIB_PATH):
                                    f"(or __graft_entry__.build()) first")
             lib = ctypes.CDLL(path)
             for name, (res, args) in EXPORTS.items():
+                if override and not hasattr(lib, name) and ("_set_" in name or "describe" in name):
+                    continue
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
@@ -490,6 +498,45 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
     return out
 
 
+PLAN_KINDS = {0: "tile", 1: "halo", 2: "wide", 3: "ars", 4: "big"}
+
+
+def describe_plan(batch, h, w, c0, n, *, c1=0, ksize=3, stride=1, upsample=False, out_layout=OUT_NHWC,
+                  dtype=torch.bfloat16, residual=False, temb=False, gn_stats=False, row_stats=False, ln=False,
+                  act=ACT_NONE, geglu_bias=True):
+    """The kernel / tile plan ldm_conv2d picks for a call of this shape (host only: the library's
+    planner on a parameter block with placeholder 16-byte-aligned addresses; nothing launches).
+    Returns {"kind", "bm", "bn", "ksplit", "stages", "blocks"}."""
+    lib = load_library()
+    fake = ctypes.c_void_p(1 << 20)
+    ce = 16 // (4 if dtype == torch.float32 else 2)
+    c0p = (c0 + ce - 1) // ce * ce
+    k = ksize
+    if k == 1:
+        ho, wo = h, w
+    elif upsample:
+        ho, wo = 2 * h, 2 * w
+    else:
+        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+    M = batch * ho * wo
+    p = ConvParams(fake, fake if c1 else None, c0p, c1, batch, h, w, ho, wo, k, stride, int(upsample), fake, n,
+                   _kpad(k * k * (c0p + c1)), fake if geglu_bias else None, fake if temb else None, n if temb else 0,
+                   fake if residual else None, fake, out_layout, act, dtype_code(dtype), 0, None, 0,
+                   fake if gn_stats else None, 0, gn_unit_for(n) if gn_stats else 0,
+                   gn_slots_for(ho * wo) if gn_stats else 0, fake if row_stats else None, fake if ln else None,
+                   fake if ln else None, 1.0 / (c0p + c1) if ln else 0.0, 1e-5 if ln else 0.0)
+    out = (ctypes.c_int * 5)()
+    _check(lib.ldm_conv2d_describe_plan(ctypes.byref(p), out), "ldm_conv2d_describe_plan")
+    kind, bm, bn, ks, st = list(out)
+    if kind == 0 or kind == 4:
+        blocks = -(-M // bm) * -(-n // bn) * ks
+    elif kind == 1:
+        blocks = M // bm * (n // bn)
+    else:
+        blocks = -(-M // bm) * (n // bn) if bn else None
+    return {"kind": PLAN_KINDS[kind], "bm": bm, "bn": bn, "ksplit": ks, "stages": st, "blocks": blocks}
+
+
 def softmax_rows(s, n, scale, dtype):
     """s fp32 [rows, stride] (GPU) -> softmax over the first n columns of scale * s, zeros in
     columns [n, stride); output dtype fp32 or bf16."""
@@ -514,6 +561,12 @@ def set_attention_maxcol(mode=2):
     """Tuning hook (head_dim 40): 2 the 32x32x16 kernel (default), 1 the 16x16x32 kernel with the
     scale and running max in the Q.K^T padding, 0 the 16x16x32 kernel with an FMA per score."""
     load_library().ldm_attention_set_maxcol(int(mode))
+
+
+def set_attention_bwd32(enabled=True):
+    """Tuning / A-B hook: the bf16 attention backward (head_dim <= 64) on the 32x32x16 MFMA kernels
+    (default) or the 16x16x16 ones."""
+    load_library().ldm_attention_set_bwd32(int(bool(enabled)))
 
 
 def force_attention_legacy(legacy=True):
