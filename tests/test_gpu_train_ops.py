@@ -42,6 +42,8 @@ CONV_CASES = [
     (2, 8, 8, 64, 0, 64, 3, 1, True),           # Upsample2D (nearest-2x + conv)
     (3, 7, 9, 128, 64, 72, 1, 1, False),        # 1x1 shortcut on a concat
     (1, 5, 5, 16, 0, 320, 3, 1, False),         # conv_in-like (few input channels)
+    (4, 32, 32, 320, 0, 320, 3, 1, False),      # many 64-pixel stages per split (L2-touch pipeline)
+    (2, 32, 32, 128, 64, 160, 3, 1, False),     # the same with a concat source and a ragged tile
 ]
 
 

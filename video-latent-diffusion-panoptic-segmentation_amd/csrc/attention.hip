@@ -1409,6 +1409,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv32(const AttnBwdArgs p) {
           dvt[db] = mma32(tr_a32<ROW>(Ds, qb, st, db, lane), pb[st], dvt[db]);   // dV^T += dO^T P
           dkt[db] = mma32(tr_a32<ROW>(Qs, qb, st, db, lane), zb[st], dkt[db]);   // dK^T += Q^T dZ
         }
+      // one query block's S / dP live at a time (occupancy: kres.py)
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 
@@ -1524,6 +1526,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q32(const AttnBwdArgs p) {
       for (int db = 0; db < NDB; ++db)
 #pragma unroll
         for (int st = 0; st < 2; ++st) dqt[db] = mma32(tr_a32<ROW>(Ks, kb, st, db, lane), zb[st], dqt[db]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   };
 

@@ -39,7 +39,18 @@ struct WgArgs {
   int n, kpad, K, M;
   int tiles_n, splits;
   float* part;                  // [splits][n][kpad]
+  float inv_hw, inv_w;          // 1 / hw_out, 1 / w_out (pixel decode by reciprocal, M < 2^24)
 };
+
+// q = x / d, r = x % d for 0 <= x < 2^24 from a float reciprocal (|x * inv - x / d| < 1, one
+// correction step): ~8 VALU instead of an integer division's ~30 — the wgrad loader decodes 4
+// pixels per lane per 64-pixel stage
+__device__ __forceinline__ void fdivmod(int x, int d, float inv, int& q, int& r) {
+  q = (int)((float)x * inv);
+  r = x - q * d;
+  if (r < 0) { --q; r += d; }
+  else if (r >= d) { ++q; r -= d; }
+}
 
 constexpr int WG_MB = 64;        // pixel rows per stage
 constexpr int WG_IMG = WG_MB * 256;
@@ -133,8 +144,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
       const void* sd = (mok && nval) ? (const void*)(p.dy + ((int64_t)m * p.n + ncol) * ES) : (const void*)&kZero16;
       const void* sx = &kZero16;
       if (mok && kval) {
+#ifdef LDM_WG_INTDIV
         const int b = m / p.hw_out, pix = m - b * p.hw_out;
         const int oy = pix / p.w_out, ox = pix - oy * p.w_out;
+#else
+        int b, pix, oy, ox;
+        fdivmod(m, p.hw_out, p.inv_hw, b, pix);
+        fdivmod(pix, p.w_out, p.inv_w, oy, ox);
+#endif
         const int uy = (p.upsample ? oy : oy * p.stride) - p.pad + ky;
         const int ux = (p.upsample ? ox : ox * p.stride) - p.pad + kx;
         if ((unsigned)uy < (unsigned)hin_v && (unsigned)ux < (unsigned)win_v) {
@@ -889,6 +906,7 @@ int wgrad_validate(const ldm_wgrad_params* q, int* es_out, int* M_out) {
   if (q->batch <= 0 || q->h_in <= 0 || q->w_in <= 0 || q->h_out <= 0 || q->w_out <= 0) return LDM_ERR_ARG;
   if (q->c0 <= 0 || q->c1 < 0 || (q->c1 > 0 && !q->a1)) return LDM_ERR_ARG;
   if (q->c0 % ce || q->c1 % ce || q->n % ce) return LDM_ERR_ALIGN;
+  if ((int64_t)q->batch * q->h_out * q->w_out >= (1 << 24)) return LDM_ERR_ARG;   // reciprocal pixel decode
   const int cin = q->c0 + q->c1;
   if (q->kpad % 64 || q->ksize * q->ksize * cin > q->kpad || q->n <= 0) return LDM_ERR_ARG;
   if (q->cin_real <= 0 || q->cin_real > cin) return LDM_ERR_ARG;
@@ -934,6 +952,8 @@ extern "C" int ldm_conv2d_wgrad(const ldm_wgrad_params* q, ldm_stream_t stream) 
   a.dy = static_cast<const char*>(q->dy);
   a.n = q->n; a.kpad = q->kpad; a.K = q->ksize * q->ksize * a.cin; a.M = M;
   a.tiles_n = tiles_n; a.splits = sp;
+  a.inv_hw = 1.0f / (float)a.hw_out;
+  a.inv_w = 1.0f / (float)a.w_out;
   a.part = static_cast<float*>(q->workspace);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int blocks = tiles_n * tiles_k * sp;

@@ -54,22 +54,6 @@ constexpr int SCR_C1 = 512, SCR_ROW = 1024;
 constexpr int NST = FM * FN / 2;            // epilogue store instructions per lane (20)
 }  // namespace wide
 
-// One byte per lane global -> LDS (M0 + lane): an L2 prefetch of the lane's line that needs no
-// destination VGPR (a register load would leave a late write the compiler does not know about).
-// Counted on vmcnt like the operand DMA.
-__device__ __forceinline__ void touch1(__amdgpu_buffer_rsrc_t rsrc, int voff, unsigned lds_addr) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_ubyte %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
-      : "memory");
-}
-
 // GEGLU: the epilogue form (one instantiation per form)
 template <bool GEGLU>
 __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
@@ -108,6 +92,9 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   const __amdgpu_buffer_rsrc_t ra1 =
       __builtin_amdgcn_make_buffer_rsrc((void*)(p.a1 ? p.a1 : p.a0), 0, p.a1 ? p.a1_bytes : 0, kBufFlags);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, p.w_bytes, kBufFlags);
+#ifdef LDM_ABL_NO_PREFETCH
+  const __amdgpu_buffer_rsrc_t rnone = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, 0, 0, kBufFlags);
+#endif
   const __amdgpu_buffer_rsrc_t rbias =
       __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, 0, p.bias ? p.n * 4 : 0, kBufFlags);
   const __amdgpu_buffer_rsrc_t rc1 =
@@ -169,9 +156,6 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   // touch (L2 prefetch) the operand lines of K tile s: line L = 72 wv + 64 i + lane < 72 (wv + 1);
   // L < 256: A row m0 + L, else B row n0 + L - 256 (one 128-B line each)
   auto prefetch = [&](int s) {
-#ifdef LDM_ABL_NO_PREFETCH
-    return;
-#endif
     const int r = s / nks, kt = s - r * nks;
     int m0, n0;
     coords(r, m0, n0);
@@ -195,8 +179,13 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
       }
       // the A and B lines of one instruction may both occur: two loads, each with the other's lanes
       // out of range (no memory access)
+#ifdef LDM_ABL_NO_PREFETCH   // ablation build: the same counted instructions on empty descriptors
+      touch1(rnone, off_a, pf0);
+      touch1(rnone, off_b, pf0);
+#else
       touch1(sel ? ra1 : ra0, off_a, pf0);
       touch1(rw, off_b, pf0);
+#endif
     }
   };
 

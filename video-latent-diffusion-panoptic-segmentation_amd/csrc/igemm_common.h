@@ -125,6 +125,22 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, int voff, uns
       : "memory");
 }
 
+// One byte per lane global -> LDS (M0 + lane): an L2 prefetch of the lane's line that needs no
+// destination VGPR (a register load would leave a late write the compiler does not know about).
+// Counted on vmcnt like the operand DMA; an out-of-range offset (kOOB) makes no memory access.
+__device__ __forceinline__ void touch1(__amdgpu_buffer_rsrc_t rsrc, int voff, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_ubyte %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(__builtin_amdgcn_readfirstlane(lds_addr))
+      : "memory");
+}
+
 template <typename T>
 __device__ __forceinline__ void store4(char* base, int64_t idx, const float* v, bool f32out) {
   if (f32out || sizeof(T) == 4) {
