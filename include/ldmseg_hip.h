@@ -163,10 +163,17 @@ typedef struct {
 
 int ldm_attention(const ldm_attn_params* p, ldm_stream_t stream);
 /* BASELINE config 5 ("fp8 MFMA attention", pose-conditioned video LDM at T=16): as ldm_attention
- * (bf16 only), with the P.V product on the e4m3 MFMA — P and V rounded to OCP e4m3, fp32
- * accumulation; Q.K^T and the softmax in bf16 / fp32.  Accuracy mode: on gfx950 the non-scaled
- * fp8 MFMA issues at the bf16 rate. */
-int ldm_attention_fp8(const ldm_attn_params* p, ldm_stream_t stream);
+ * (bf16 inputs and output).
+ *   head_dim 40 (16-byte row strides): BOTH products on the block-scaled
+ *     v_mfma_scale_f32_32x32x64_f8f6f4 (2x the bf16 MFMA rate) — Q * scale * log2(e), K, V and P
+ *     rounded to OCP e4m3 (unit E8M0 scales), fp32 accumulation, softmax in fp32.  K and V are
+ *     quantized once per call into the caller's workspace (ldm_attention_fp8_workspace_bytes).
+ *   other head dims: P.V on the non-scaled e4m3 MFMA (issues at the bf16 rate on gfx950; an
+ *     accuracy mode), Q.K^T bf16; the workspace is unused (may be NULL). */
+size_t ldm_attention_fp8_workspace_bytes(const ldm_attn_params* p);
+int ldm_attention_fp8(const ldm_attn_params* p, void* workspace, int64_t workspace_bytes, ldm_stream_t stream);
+/* Tuning / A-B hook: 0 sends head_dim 40 to the non-scaled P.V path as well (default 1). */
+void ldm_attention_set_fp8_scaled(int enabled);
 /* Tuning hook (benchmarks / tests only): 1 routes bf16 through the 16x16x16-MFMA kernel
  * instead of the 16x16x32 one; 0 restores the default. */
 void ldm_attention_force_legacy(int legacy);

@@ -48,11 +48,14 @@ def test_unet_sd14_t16_32x64_matches_oracle():
 
 @pytest.mark.parametrize("N,C", [(2048, 320), (4096, 320), (512, 640), (128, 1280), (100, 320)])
 def test_fp8_attention_within_stated_tolerance(N, C):
-    """ldm_attention_fp8 (P.V on e4m3) against torch fp32 attention on the same bf16 inputs.
-    Bar: relative L2 error <= 5e-2 and max-abs error <= 1.5e-1 of the output's max-abs.  e4m3
-    keeps 3 mantissa bits (relative rounding <= 2^-4, RMS ~3.6 % for uniform mantissas); with a
-    flat softmax the output is a mean of V and its rounding errors shrink with the output itself,
-    so the relative error stays at the e4m3 level (measured 3.7e-2 at N=2048, bf16 2.1e-3)."""
+    """ldm_attention_fp8 against torch fp32 attention on the same bf16 inputs (x 1.5: peakier than
+    the UNet's).  head_dim 80 / 160 (P.V on e4m3): relative L2 error <= 5e-2 and max-abs error <=
+    1.5e-1 of the output's max-abs — e4m3 keeps 3 mantissa bits (relative rounding <= 2^-4, RMS
+    ~3.6 % for uniform mantissas), and with a flat softmax the output is a mean of V whose rounding
+    errors shrink with it (measured 3.7e-2 at N=2048, bf16 2.1e-3).  head_dim 40 (Q.K^T in e4m3 as
+    well, the block-scaled kernel): every score then carries the rounding of 40 e4m3 products
+    (~7 % RMS each, ~0.16 absolute on scores of spread 2.25 here), so the bar is rel-L2 <= 1e-1 and
+    max <= 2e-1."""
     heads, B = 8, 2
     d = C // heads
     g = torch.Generator(device=DEV).manual_seed(N + C)
@@ -66,7 +69,34 @@ def test_fp8_attention_within_stated_tolerance(N, C):
     bf = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, d, N, N, 3 * C, 3 * C, 3 * C)
     l2_bf16 = ((bf.float() - ref).norm() / ref.norm()).item()
     print(f"N={N} C={C}: fp8 rel-L2 {l2:.3e} max {mx:.3e}; bf16 rel-L2 {l2_bf16:.3e}")
-    assert l2 <= 5e-2 and mx <= 1.5e-1
+    if d in K.FP8_SCALED_HEAD_DIMS:
+        assert l2 <= 1e-1 and mx <= 2e-1
+    else:
+        assert l2 <= 5e-2 and mx <= 1.5e-1
+
+
+@pytest.mark.parametrize("N,B", [(2048, 2), (4096, 1), (100, 2), (64 * 33 + 5, 1)])
+def test_fp8_scaled_attention_d40(N, B):
+    """head_dim 40 on the block-scaled MFMA kernel (Q.K^T and P.V in e4m3): against torch fp32
+    attention on the same bf16 inputs, and against the non-scaled fp8 path (P.V only).  Inputs at
+    the scale of the UNet's LayerNorm'd projections; ragged N exercises the masked last key tile.
+    Bar: rel-L2 <= 6e-2 (both operands of both products rounded to 3 mantissa bits)."""
+    C, heads = 320, 8
+    g = torch.Generator(device=DEV).manual_seed(N)
+    qkv = torch.randn(B, N, 3 * C, device=DEV, generator=g).to(torch.bfloat16)
+    x = qkv.float().view(B, N, 3, heads, 40).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(x[0] @ x[1].transpose(-1, -2) * 40 ** -0.5, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B, N, C)
+    out = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, 40, N, N, 3 * C, 3 * C, 3 * C, fp8=True)
+    K.set_attention_fp8_scaled(False)
+    try:
+        old = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, 40, N, N, 3 * C, 3 * C, 3 * C, fp8=True)
+    finally:
+        K.set_attention_fp8_scaled(True)
+    l2 = ((out.float() - ref).norm() / ref.norm()).item()
+    l2_old = ((old.float() - ref).norm() / ref.norm()).item()
+    print(f"N={N}: scaled fp8 rel-L2 {l2:.3e}, P.V-only fp8 {l2_old:.3e}")
+    assert torch.isfinite(out.float()).all()
+    assert l2 <= 6e-2
 
 
 def test_unet_config5_fp8_attention_close_to_oracle():

@@ -49,14 +49,16 @@ def mm_case(M, K, N):
     return (lambda: torch.mm(a, b)), 2.0 * M * K * N, None
 
 
-def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2):
+def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
     def run():
         K.force_attention_legacy(legacy)
         K.set_attention_waves(waves)
         K.set_attention_maxcol(maxcol)
-        return K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, C // heads, N, N, 3 * C, 3 * C, 3 * C)
+        K.set_attention_fp8_scaled(scaled)
+        return K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, C // heads, N, N, 3 * C, 3 * C, 3 * C,
+                           fp8=fp8)
     return run, 4.0 * B * heads * N * N * (C // heads), None
 
 
@@ -169,6 +171,10 @@ CASES = {
     "mm_conv_l2_1280": lambda: mm_case(2048, 11520, 1280),
     "mm_conv_l3_1280": lambda: mm_case(512, 11520, 1280),
     "attn_4096_d40": lambda: attn_case(8, 4096, 320),
+    "attn_c5_2048_d40": lambda: attn_case(16, 2048, 320),
+    "attn_c5_2048_d40_fp8": lambda: attn_case(16, 2048, 320, fp8=True),
+    "attn_c5_2048_d40_fp8pv": lambda: attn_case(16, 2048, 320, fp8=True, scaled=False),
+    "attn_4096_d40_fp8": lambda: attn_case(8, 4096, 320, fp8=True),
     "attn_4096_d40_fma": lambda: attn_case(8, 4096, 320, maxcol=0),
     "attn_4096_d40_mc16": lambda: attn_case(8, 4096, 320, maxcol=1),
     "attn_1024_d80_fma": lambda: attn_case(8, 1024, 640, maxcol=0),

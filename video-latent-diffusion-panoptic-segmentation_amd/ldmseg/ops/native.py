@@ -71,7 +71,9 @@ EXPORTS = {
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
-    "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp]),
+    "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp, _i64, _vp]),
+    "ldm_attention_fp8_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
+    "ldm_attention_set_fp8_scaled": (None, [_i]),
     "ldm_attention_set_maxcol": (None, [_i]),
     "ldm_group_norm_workspace_bytes": (ctypes.c_size_t, [_i, _i, _i]),
     "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _i, _i, _vp, _i, _vp]),
@@ -563,6 +565,15 @@ def set_attention_maxcol(mode=2):
     load_library().ldm_attention_set_maxcol(int(mode))
 
 
+FP8_SCALED_HEAD_DIMS = (40,)     # ldm_attention_fp8's block-scaled MFMA kernel (others: non-scaled P.V)
+
+
+def set_attention_fp8_scaled(enabled=True):
+    """Tuning / A-B hook: head_dim 40 fp8 attention on the block-scaled MFMA kernel (default) or on the
+    non-scaled P.V path."""
+    load_library().ldm_attention_set_fp8_scaled(int(bool(enabled)))
+
+
 def set_attention_bwd32(enabled=True):
     """Tuning / A-B hook: the bf16 attention backward (head_dim <= 64) on the 32x32x16 MFMA kernels
     (default) or the 16x16x16 ones."""
@@ -632,7 +643,8 @@ def linear(pc: PackedConv, x, **kw):
 # ======================================================================================
 def attention(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_stride, out=None, scale=None,
               fp8=False):
-    """fp8=True: ldm_attention_fp8 (P.V on the e4m3 MFMA; bf16 inputs only)."""
+    """fp8=True: ldm_attention_fp8 (head_dim 40: Q.K^T and P.V on the block-scaled e4m3 MFMA; other
+    head dims: P.V on the non-scaled e4m3 MFMA; bf16 inputs only)."""
     lib = load_library()
     _gpu(q, k, v, out)
     C = heads * head_dim
@@ -650,7 +662,9 @@ def attention(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_
     if fp8:
         if q.dtype != torch.bfloat16:
             raise TypeError("fp8 attention takes bf16 q/k/v")
-        _check(lib.ldm_attention_fp8(ctypes.byref(p), _stream(q)), "ldm_attention_fp8")
+        wsb = int(lib.ldm_attention_fp8_workspace_bytes(ctypes.byref(p)))
+        ws = torch.empty(wsb, dtype=torch.uint8, device=q.device) if wsb else None
+        _check(lib.ldm_attention_fp8(ctypes.byref(p), _ptr(ws), wsb, _stream(q)), "ldm_attention_fp8")
     else:
         _check(lib.ldm_attention(ctypes.byref(p), _stream(q)), "ldm_attention")
     _prof_stop(ev, "attention", 4.0 * batch * heads * n_q * n_kv * head_dim,
