@@ -401,6 +401,9 @@ typedef struct {
 } ldm_wgrad_params;
 size_t ldm_conv2d_wgrad_workspace_bytes(const ldm_wgrad_params* p);
 int ldm_conv2d_wgrad(const ldm_wgrad_params* p, ldm_stream_t stream);
+/* Tuning / A-B hook: 1 (default) runs the bf16 weight gradient on a ring of four 32-pixel LDS
+ * stages (three in flight), 0 on two 64-pixel stages. */
+void ldm_conv2d_wgrad_set_ring(int ring);
 
 /* ldm_colsum — out[s][c] (+)= sum over the rows of segment s of x[rows][c] (segments split the
  * rows evenly).  Bias gradients (1 segment) and per-batch time-embedding gradients (batch

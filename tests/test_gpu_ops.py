@@ -225,7 +225,7 @@ def test_attention(B, N, L, C, dt):
 
 @pytest.mark.parametrize("waves", [0, 4, 8])
 @pytest.mark.parametrize("B,N,C", [(2, 4096, 320), (2, 1024, 640), (1, 300, 320), (2, 520, 640), (16, 1024, 320),
-                                   (16, 1000, 320)])
+                                   (16, 1000, 320), (1, 4096, 320)])
 def test_attention_block_waves(B, N, C, waves):
     """Every block shape of the bf16 kernel (4 or 8 waves sharing each K/V tile; waves=0 lets
     the launcher pick, which at head_dim 40 with >= 512 blocks is two 8-wave blocks per CU of

@@ -62,7 +62,7 @@ def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scal
     return run, 4.0 * B * heads * N * N * (C // heads), None
 
 
-def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False):
+def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False, ring=True):
     g = torch.Generator(device=DEV).manual_seed(0)
     x = torch.randn(B, H, W, Cin, device=DEV, generator=g).to(BF)
     dy = torch.randn(B, H, W, Cout, device=DEV, generator=g).to(BF)
@@ -71,6 +71,7 @@ def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False):
     dw = torch.empty(Cout, Cin, k, k, device=DEV) if k == 3 else torch.empty(Cout, Cin, device=DEV)
 
     def run():
+        K.set_wgrad_ring(ring)
         return K.conv2d_wgrad(pc, x, B, H, W, dy, dw=dw)
     return run, 2.0 * B * H * W * Cout * k * k * Cin, None
 
@@ -195,6 +196,12 @@ CASES = {
     "wgrad_ff2_1280": lambda: wgrad_case(16, 64, 64, 1280, 320, k=1),
     "wgrad_proj_320": lambda: wgrad_case(16, 64, 64, 320, 320, k=1),
     "wgrad_qkv_320": lambda: wgrad_case(16, 64, 64, 320, 960, k=1),
+    "wgrad_l0_320_old": lambda: wgrad_case(16, 64, 64, 320, 320, ring=False),
+    "wgrad_l1_640_old": lambda: wgrad_case(16, 32, 32, 640, 640, ring=False),
+    "wgrad_l2_1280_old": lambda: wgrad_case(16, 16, 16, 1280, 1280, ring=False),
+    "wgrad_up_960_old": lambda: wgrad_case(16, 64, 64, 960, 320, ring=False),
+    "wgrad_geglu_320_old": lambda: wgrad_case(16, 64, 64, 320, 2560, k=1, geglu=True, ring=False),
+    "wgrad_qkv_320_old": lambda: wgrad_case(16, 64, 64, 320, 960, k=1, ring=False),
     "attn_bwd_4096_d40": lambda: attn_bwd_case(16, 4096, 320),
     "attn_bwd_4096_d40_old": lambda: attn_bwd_case(16, 4096, 320, new=False),
     "attn_bwd_1024_d80": lambda: attn_bwd_case(16, 1024, 640),

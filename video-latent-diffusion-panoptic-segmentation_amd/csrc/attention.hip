@@ -893,6 +893,8 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
       } else if (nblk >= 512 || g_attn_waves == 8) hipLaunchKernelGGL((attn_d40_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a);
       else {
         const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
+        // (2-wave blocks of 64 queries for a single frame were measured slower: B = 1, N = 4096
+        // 0.74 -> 1.07 ms for the step's five launches — each K/V tile then serves 64 queries)
         hipLaunchKernelGGL((attn_d40_kernel<4, 2>), dim3(nb4), dim3(256), 0, s, a);
       }
       LDM_CHECK_LAUNCH();

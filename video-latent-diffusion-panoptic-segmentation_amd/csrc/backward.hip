@@ -52,8 +52,6 @@ __device__ __forceinline__ void fdivmod(int x, int d, float inv, int& q, int& r)
   else if (r >= d) { ++q; r -= d; }
 }
 
-constexpr int WG_MB = 64;        // pixel rows per stage
-constexpr int WG_IMG = WG_MB * 256;
 
 // XOR swizzle of the 16 16-byte chunks of a 256-byte row: serves the transposed fragment
 // reads (and row reads) conflict-free (cdna_hip_programming.md T10 image (b)).
@@ -97,11 +95,18 @@ __device__ __forceinline__ Frag8<float> wg_frag<float>(const char* img, int r0, 
 
 // One block = one [TE n] x [TE k] tile of dW over one pixel range.  TE = 128 (bf16) / 64 (fp32),
 // i.e. 256-byte image rows.  4 waves as 2 (n) x 2 (k), wave tile TE/2 x TE/2.
-template <typename T>
+// Stages of MB pixels in an NS-slot LDS ring.  The main loop is bound by operand latency, not by
+// the MFMA or the LDS reads (ablation builds, profiles/r03_r3j_wgrad.txt: loads removed 410 -> 152
+// us, MFMAs removed 410 -> 364 us at the 64x64-level 3x3 320): with one 32-KB 64-pixel stage in
+// flight per block (NS = 2) every stage waits out a memory round trip.  The bf16 default is a ring of
+// four 32-pixel stages (16 KB each, three in flight, counted vmcnt and a raw barrier per stage).
+template <typename T, int MB, int NS>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
   constexpr int ES = sizeof(T), EPC = 16 / ES;
   constexpr int TE = 256 / ES, WT = TE / 2, NF = WT / 16;
-  __shared__ uint4 smem[2 * 2 * WG_IMG / 16];
+  constexpr int IMG = MB * 256;                  // bytes per operand image of one stage
+  constexpr int PER = 2 * (MB / 16);             // DMA instructions per wave and stage
+  __shared__ uint4 smem[NS * 2 * IMG / 16];
   typedef __attribute__((address_space(3))) uint4 lds_u4_t;
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
   const char* sbase = reinterpret_cast<const char*>(smem);
@@ -131,14 +136,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
   const int cof = s1 ? c - p.c0 : c;
   const int hin_v = p.upsample ? 2 * p.h_in : p.h_in, win_v = p.upsample ? 2 * p.w_in : p.w_in;
 
-  auto issue = [&](int mb, int buf) {
+  auto issue = [&](int mb, int slot) {
 #ifdef LDM_ABL_NO_LOADS
     return;
 #endif
-    const unsigned dyb = lds0 + (unsigned)(buf * 2 * WG_IMG);
-    const unsigned xb = dyb + WG_IMG;
+    const unsigned dyb = lds0 + (unsigned)(slot * 2 * IMG);
+    const unsigned xb = dyb + IMG;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MB / 16; ++i) {
       const int m = mb + 16 * i + rlow;
       const bool mok = m < m_hi;
       const void* sd = (mok && nval) ? (const void*)(p.dy + ((int64_t)m * p.n + ncol) * ES) : (const void*)&kZero16;
@@ -172,11 +177,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  auto compute = [&](int buf) {
-    const char* dyi = sbase + buf * 2 * WG_IMG;
-    const char* xi = dyi + WG_IMG;
+  auto compute = [&](int slot) {
+    const char* dyi = sbase + slot * 2 * IMG;
+    const char* xi = dyi + IMG;
 #pragma unroll
-    for (int s = 0; s < WG_MB / 32; ++s) {
+    for (int s = 0; s < MB / 32; ++s) {
       Frag8<T> af[NF], bf[NF];
 #pragma unroll
       for (int i = 0; i < NF; ++i) af[i] = wg_frag<T>(dyi, 32 * s, wn * WT + 16 * i, lane);
@@ -197,15 +202,35 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
   };
 
   if (m_lo < m_hi) {
-    issue(m_lo, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    int it = 0;
-    for (int mb = m_lo; mb < m_hi; mb += WG_MB, ++it) {
-      const int buf = it & 1;
-      if (mb + WG_MB < m_hi) issue(mb + WG_MB, buf ^ 1);
-      compute(buf);
+    const int nst = (m_hi - m_lo + MB - 1) / MB;
+    if constexpr (NS == 2) {
+      issue(m_lo, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int st = 0; st < nst; ++st) {
+        const int slot = st & 1;
+        if (st + 1 < nst) issue(m_lo + (st + 1) * MB, slot ^ 1);
+        compute(slot);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    } else {
+      static_assert(NS == 4, "ring depth");
+#pragma unroll
+      for (int i = 0; i < NS - 1; ++i)
+        if (i < nst) issue(m_lo + i * MB, i);
+      for (int st = 0; st < nst; ++st) {
+        // stage st landed for this wave; the (up to two) younger stages may stay in flight
+        const int ahead = min(NS - 2, nst - 1 - st);
+        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+        else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // raw barrier (__syncthreads would drain the stages in flight): every wave's part of stage st
+        // is in LDS and every wave is done with the slot stage st + 3 reuses (stage st - 1's)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (st + NS - 1 < nst) issue(m_lo + (st + NS - 1) * MB, (st + NS - 1) % NS);
+        compute(st % NS);
+      }
       __syncthreads();
     }
   }
@@ -925,6 +950,11 @@ int wgrad_validate(const ldm_wgrad_params* q, int* es_out, int* M_out) {
 
 }  // namespace
 
+namespace {
+int g_wgrad_ring = 1;   // tuning / A-B hook (ldm_conv2d_wgrad_set_ring): 0 = two 64-pixel stages
+}  // namespace
+extern "C" void ldm_conv2d_wgrad_set_ring(int ring) { g_wgrad_ring = ring ? 1 : 0; }
+
 extern "C" size_t ldm_conv2d_wgrad_workspace_bytes(const ldm_wgrad_params* q) {
   int es = 0, M = 0;
   if (wgrad_validate(q, &es, &M) != LDM_OK) return 0;
@@ -957,8 +987,9 @@ extern "C" int ldm_conv2d_wgrad(const ldm_wgrad_params* q, ldm_stream_t stream) 
   a.part = static_cast<float*>(q->workspace);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int blocks = tiles_n * tiles_k * sp;
-  if (q->dtype == LDM_BF16) hipLaunchKernelGGL(wgrad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL(wgrad_kernel<float>, dim3(blocks), dim3(256), 0, s, a);
+  if (q->dtype == LDM_BF16 && g_wgrad_ring) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 32, 4>), dim3(blocks), dim3(256), 0, s, a);
+  else if (q->dtype == LDM_BF16) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 64, 2>), dim3(blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((wgrad_kernel<float, 64, 2>), dim3(blocks), dim3(256), 0, s, a);
   LDM_CHECK_LAUNCH();
   const int64_t total = (int64_t)q->n * q->kpad;
   hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a.part, sp, q->n, q->kpad,

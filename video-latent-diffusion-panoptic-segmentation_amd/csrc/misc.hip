@@ -405,7 +405,7 @@ __device__ __forceinline__ int geglu_src_row(int p, int half) {   // packed (int
 // stride of ci * 9 floats: 9.4 ms of a 142 ms training iteration, profiles/r03a_train_*).
 constexpr int RP_R = 16, RP_C = 64, RP_MAXT = 9, RP_VEC = 2048;
 __global__ __launch_bounds__(256) void repack_kernel(const ldm_repack_desc* __restrict__ d, int nd, int64_t total) {
-  __shared__ float lds[RP_R * RP_C * RP_MAXT];
+  __shared__ __attribute__((aligned(16))) float lds[RP_R * RP_C * RP_MAXT];
   const int64_t q = blockIdx.x;
   if (q >= total) return;
   int lo = 0, hi = nd - 1;
@@ -430,20 +430,39 @@ __global__ __launch_bounds__(256) void repack_kernel(const ldm_repack_desc* __re
   // LDS image: fwd  lds[i][jj * T + t] = W[row'(r0 + i)][c0 + jj][t]        (run 64 T per source row)
   //            dgrad lds[jj][i * T + t] = W[c'(c0 + jj)][r0 + i][t]          (run 16 T per source row)
   const int nsrc = fwd ? RP_R : RP_C, run = fwd ? RP_C * T : RP_R * T;
-  for (int idx = tid; idx < nsrc * run; idx += 256) {
-    const int sr = idx / run, x = idx - sr * run;
-    float v = 0.f;
+  // source row sr's run starts at run_base(sr) (float index, or -1: a zero row) and holds `lim`
+  // valid floats (the channel range is clipped at ci)
+  auto run_base = [&](int sr, int& lim) -> int64_t {
     if (fwd) {
       const int r = r0 + sr;
       const int co = e.geglu ? geglu_src_row(r, e.co >> 1) : r;
-      if (r < e.rows && co < e.co && c0 * T + x < e.ci * T)
-        v = src[((int64_t)co * e.ci + c0) * T + x];
-    } else {
-      const int c = c0 + sr;
-      const int co = e.geglu ? geglu_src_row(c, e.co >> 1) : c;
-      if (c < e.co && r0 * T + x < e.ci * T) v = src[((int64_t)co * e.ci + r0) * T + x];
+      lim = (e.ci - c0) * T;
+      return (r < e.rows && co < e.co) ? ((int64_t)co * e.ci + c0) * T : -1;
     }
-    lds[idx] = v;
+    const int c = c0 + sr;
+    const int co = e.geglu ? geglu_src_row(c, e.co >> 1) : c;
+    lim = (e.ci - r0) * T;
+    return c < e.co ? ((int64_t)co * e.ci + r0) * T : -1;
+  };
+  if ((e.ci * T) % 4 == 0) {
+    // 16-byte loads: every run starts 16-byte aligned (c0 * T, r0 * T and ci * T are multiples of 4)
+    // and is a whole number of float4; independent loads, all in flight
+    const int run4 = run / 4;
+    for (int idx = tid; idx < nsrc * run4; idx += 256) {
+      const int sr = idx / run4, x = 4 * (idx - sr * run4);
+      int lim;
+      const int64_t b = run_base(sr, lim);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (b >= 0 && x < lim) v = *reinterpret_cast<const float4*>(src + b + x);
+      *reinterpret_cast<float4*>(lds + sr * run + x) = v;
+    }
+  } else {
+    for (int idx = tid; idx < nsrc * run; idx += 256) {
+      const int sr = idx / run, x = idx - sr * run;
+      int lim;
+      const int64_t b = run_base(sr, lim);
+      lds[idx] = (b >= 0 && x < lim) ? src[b + x] : 0.f;
+    }
   }
   __syncthreads();
   // writes: item (i, tap, g) = destination row r0 + i, columns tap * cpad + c0 + 8 g .. + 7

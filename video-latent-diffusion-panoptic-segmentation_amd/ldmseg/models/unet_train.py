@@ -282,14 +282,24 @@ class UNetTrainGraph:
                         3 * C, dqkv, dqkv[..., C:], dqkv[..., 2 * C:], 3 * C, 3 * C)
         # fused QKV projection
         if a1.to_q.weight.requires_grad:
-            wq = torch.empty(3 * C, C, dtype=torch.float32, device=qkv.device)
-            K.conv2d_wgrad(p["qkv"], s["n1"], M, 1, 1, dqkv, dw=wq)
-            for i, lin in enumerate((a1.to_q, a1.to_k, a1.to_v)):
-                dst, accq = self.sink(lin.weight)
-                if accq:
-                    dst.add_(wq[i * C:(i + 1) * C].view_as(dst))
-                else:
-                    dst.copy_(wq[i * C:(i + 1) * C].view_as(dst))
+            sinks = [self.sink(lin.weight) for lin in (a1.to_q, a1.to_k, a1.to_v)]
+            d0 = sinks[0][0]
+            st0 = d0.untyped_storage().data_ptr()
+            adjacent = all(d.untyped_storage().data_ptr() == st0 and d.data_ptr() == d0.data_ptr() + i * d0.numel() * 4
+                           and d.is_contiguous() and a == sinks[0][1] for i, (d, a) in enumerate(sinks))
+            if adjacent:
+                # the trainer's flat buffer keeps to_q / to_k / to_v back to back: the fused [3C][C]
+                # weight gradient lands in place (no temporary, no copies)
+                dw = d0.as_strided((3 * C, C), (C, 1))
+                K.conv2d_wgrad(p["qkv"], s["n1"], M, 1, 1, dqkv, dw=dw, accumulate=sinks[0][1])
+            else:
+                wq = torch.empty(3 * C, C, dtype=torch.float32, device=qkv.device)
+                K.conv2d_wgrad(p["qkv"], s["n1"], M, 1, 1, dqkv, dw=wq)
+                for i, (dst, accq) in enumerate(sinks):
+                    if accq:
+                        dst.add_(wq[i * C:(i + 1) * C].view_as(dst))
+                    else:
+                        dst.copy_(wq[i * C:(i + 1) * C].view_as(dst))
         dn1 = self._dgrad(id(a1), dqkv, M, 1, 1)
         # norm1 (+ residual dh1)
         dg, db, acc = self._sink_pair(tb.norm1.weight, tb.norm1.bias)
@@ -370,16 +380,28 @@ class UNetTrainGraph:
         if not any(r.time_emb_proj.weight.requires_grad for r in resnets):
             return
         total = P["temb_total"]
-        dtemb = torch.zeros(self.B, total, dtype=torch.float32, device=self.dev)
-        for off, part in self.dtemb_parts.items():
-            dtemb[:, off:off + part.shape[1]] = part
+        offs = sorted(self.dtemb_parts)
+        if offs == [P[id(r), "temb_off"] for r in resnets]:       # every ResNet reported: one cat
+            dtemb = torch.cat([self.dtemb_parts[o] for o in offs], dim=1)
+        else:
+            dtemb = torch.zeros(self.B, total, dtype=torch.float32, device=self.dev)
+            for off, part in self.dtemb_parts.items():
+                dtemb[:, off:off + part.shape[1]] = part
         dy = dtemb.to(u.compute_dtype).contiguous()
         wt = K.conv2d_wgrad(P["temb_proj"], self.semb, self.B, 1, 1, dy)        # [total, 1280] fp32
         bt = K.colsum(dtemb, self.B, total).view(-1)
+        # scatter to the 22 ResNets' parameters with one multi-tensor launch per mode
+        put, add = ([], []), ([], [])
         for r in resnets:
             off, n = P[id(r), "temb_off"], r.out_channels
             for prm, val in ((r.time_emb_proj.weight, wt[off:off + n]), (r.time_emb_proj.bias, bt[off:off + n])):
                 if prm.requires_grad:
                     dst, acc = self.sink(prm)
-                    (dst.add_ if acc else dst.copy_)(val.view_as(dst))
+                    tgt = add if acc else put
+                    tgt[0].append(dst)
+                    tgt[1].append(val.view_as(dst))
+        if put[0]:
+            torch._foreach_copy_(put[0], put[1])
+        if add[0]:
+            torch._foreach_add_(add[0], add[1])
         self.on_ready([q for r in resnets for q in r.time_emb_proj.parameters() if q.requires_grad])

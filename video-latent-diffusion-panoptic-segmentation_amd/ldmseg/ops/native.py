@@ -90,6 +90,7 @@ EXPORTS = {
     "ldm_attention_fwd_lse": (_i, [ctypes.POINTER(AttnParams), _vp, _vp]),
     "ldm_attention_force_legacy": (None, [_i]),
     "ldm_attention_set_bwd32": (None, [_i]),
+    "ldm_conv2d_wgrad_set_ring": (None, [_i]),
     "ldm_attention_set_waves": (None, [_i]),
     "ldm_attention_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_bwd": (_i, [ctypes.POINTER(AttnParams), _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
@@ -572,6 +573,11 @@ def set_attention_fp8_scaled(enabled=True):
     """Tuning / A-B hook: head_dim 40 fp8 attention on the block-scaled MFMA kernel (default) or on the
     non-scaled P.V path."""
     load_library().ldm_attention_set_fp8_scaled(int(bool(enabled)))
+
+
+def set_wgrad_ring(ring=True):
+    """Tuning / A-B hook: bf16 weight gradient on four 32-pixel LDS stages (default) or two 64-pixel."""
+    load_library().ldm_conv2d_wgrad_set_ring(int(bool(ring)))
 
 
 def set_attention_bwd32(enabled=True):
