@@ -136,7 +136,23 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
   const int cof = s1 ? c - p.c0 : c;
   const int hin_v = p.upsample ? 2 * p.h_in : p.h_in, win_v = p.upsample ? 2 * p.w_in : p.w_in;
 
+  // Row walker: the lane's pixel rows are m_lo + rlow + 16 j, visited in order by successive issue()
+  // calls (4 per 64-pixel stage), so (b, oy, ox) advances by a precomputed (q16, r16) = divmod(16,
+  // w_out) instead of being decoded per row (the per-row decode was the loader's VALU bound: ~45
+  // VALU per row, more issue cycles than the stage's MFMAs).  Stride 1 without upsampling (the
+  // 3x3 / 1x1 convs but Downsample / Upsample) keeps the source pixel = row + a per-lane constant,
+  // so both operand addresses advance by one add per row.
+  int wb, wy, wx;
+  fdivmod(m_lo + rlow, p.hw_out, p.inv_hw, wb, wy);
+  { int q; fdivmod(wy, p.w_out, p.inv_w, q, wx); wy = q; }
+  const int q16 = 16 / p.w_out, r16 = 16 - q16 * p.w_out;
+  const bool plain = p.stride == 1 && !p.upsample && p.h_in == p.h_out && p.w_in == p.w_out;
+  const bool noborder = plain && p.ksize == 1;
+  // plain: source pixel = m + (ky - pad) * w_in + (kx - pad) (valid only when in bounds)
+  const int pix_shift = (ky - p.pad) * p.w_in + (kx - p.pad);
+  int mrow = m_lo + rlow;
   auto issue = [&](int mb, int slot) {
+    (void)mb;
 #ifdef LDM_ABL_NO_LOADS
     return;
 #endif
@@ -144,29 +160,33 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
     const unsigned xb = dyb + IMG;
 #pragma unroll
     for (int i = 0; i < MB / 16; ++i) {
-      const int m = mb + 16 * i + rlow;
+      const int m = mrow;
       const bool mok = m < m_hi;
       const void* sd = (mok && nval) ? (const void*)(p.dy + ((int64_t)m * p.n + ncol) * ES) : (const void*)&kZero16;
       const void* sx = &kZero16;
-      if (mok && kval) {
-#ifdef LDM_WG_INTDIV
-        const int b = m / p.hw_out, pix = m - b * p.hw_out;
-        const int oy = pix / p.w_out, ox = pix - oy * p.w_out;
-#else
-        int b, pix, oy, ox;
-        fdivmod(m, p.hw_out, p.inv_hw, b, pix);
-        fdivmod(pix, p.w_out, p.inv_w, oy, ox);
-#endif
-        const int uy = (p.upsample ? oy : oy * p.stride) - p.pad + ky;
-        const int ux = (p.upsample ? ox : ox * p.stride) - p.pad + kx;
+      if (mok && kval && noborder) {
+        sx = xs + (int64_t)m * cs + cof;                  // 1x1, stride 1: the source row is the row
+      } else if (mok && kval) {
+        const int uy = (p.upsample ? wy : wy * p.stride) - p.pad + ky;
+        const int ux = (p.upsample ? wx : wx * p.stride) - p.pad + kx;
         if ((unsigned)uy < (unsigned)hin_v && (unsigned)ux < (unsigned)win_v) {
-          const int iy = p.upsample ? (uy >> 1) : uy, ix = p.upsample ? (ux >> 1) : ux;
-          sx = xs + (((int64_t)b * p.h_in + iy) * p.w_in + ix) * cs + cof;
+          int64_t pix;
+          if (plain) pix = (int64_t)m + pix_shift;
+          else pix = ((int64_t)wb * p.h_in + (p.upsample ? (uy >> 1) : uy)) * p.w_in + (p.upsample ? (ux >> 1) : ux);
+          sx = xs + pix * cs + cof;
         }
       }
       const unsigned off = (unsigned)((16 * i + 4 * wave) * 256);
       glds16(sd, __builtin_amdgcn_readfirstlane(dyb + off));
       glds16(sx, __builtin_amdgcn_readfirstlane(xb + off));
+      // advance the walker by 16 rows
+      mrow += 16;
+      if (!noborder) {
+        wx += r16;
+        wy += q16;
+        if (wx >= p.w_out) { wx -= p.w_out; ++wy; }
+        while (wy >= p.h_out) { wy -= p.h_out; ++wb; }
+      }
     }
   };
 
