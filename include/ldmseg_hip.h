@@ -147,6 +147,22 @@ void ldm_conv2d_set_splitk_cols(int cols);
 void ldm_conv2d_set_epilogue(int mode);
 
 /* ---------------------------------------------------------------------------------------
+ * ldm_feedforward — the transformer block's FeedForward(GEGLU) as ONE launch: the two
+ * ldm_conv2d calls it replaces, passed as they would be passed separately, with the [M][F]
+ * GEGLU intermediate kept on chip (never written).
+ * Replaces: diffusers BasicTransformerBlock  hidden = ff(norm3(hidden)) + hidden  —
+ * ff.net.0 GEGLU proj + gelu gate, ff.net.2 Linear (unet.py:83-105 via 361-425).
+ *   geglu: the ff.net.0 call — 1x1, a0 = x [M][320] bf16, w = GEGLU-packed [2F][320] (16-column
+ *          hidden/gate interleave), bias packed likewise, out_layout LDM_OUT_GEGLU, out ignored
+ *          (may be NULL); optional LayerNorm fold (ln_rows / ln_c1 / ln_inv_k / ln_eps);
+ *   ff2:   the ff.net.2 call — 1x1, w = [320][F] (kpad = F = c0), bias, residual (may alias a0
+ *          and out), out [M][320], optional row_stats; a0 ignored (the intermediate).
+ * Scope: bf16, model width 320 (the 64x64 UNet level), F a multiple of 64 up to 1280; no time
+ * embedding, activation, GroupNorm partials, split-K or fp32 output.  Results equal the two
+ * separate calls bit for bit (same MFMA sequence per element, same bf16 rounding points). */
+int ldm_feedforward(const ldm_conv_params* geglu, const ldm_conv_params* ff2, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).
  * Replaces: diffusers Attention(AttnProcessor) self-attention attn1 (and cross-attention
  * attn2 when not removed, unet.py:83-105): softmax(Q K^T * scale) V per (batch, head).

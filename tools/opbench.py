@@ -90,6 +90,30 @@ def attn_bwd_case(B, N, C, heads=8, new=True):
     return run, 10.0 * B * heads * N * N * d, None     # five N x N x d matmuls (S, dP, dV, dK, dQ)
 
 
+def ff_case(rows, fused=True, Fh=1280):
+    """The transformer FeedForward at width 320 (LayerNorm-folded GEGLU + ff.net.2 + residual): the
+    fused ldm_feedforward or the two ldm_conv2d launches it replaces."""
+    C = 320
+    rows = max(128, rows * BATCH // 8)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(rows, C, device=DEV, generator=g).to(BF)
+    w1 = torch.randn(2 * Fh, C, device=DEV, generator=g) * 0.05
+    w2 = torch.randn(C, Fh, device=DEV, generator=g) * 0.03
+    pc1 = K.packed_ln_fold(w1, torch.randn(2 * Fh, device=DEV), torch.ones(C, device=DEV), torch.zeros(C, device=DEV),
+                           BF, geglu=True)
+    pc2 = K.PackedConv(w2, torch.randn(C, device=DEV), BF)
+    xd = x.double()
+    rs = torch.stack([xd.sum(-1), (xd * xd).sum(-1)], -1).reshape(-1).contiguous()
+    res = torch.randn(rows, C, device=DEV).to(BF)
+
+    def run():
+        if fused:
+            return K.feedforward(pc1, pc2, x, ln=(rs, 1e-5), residual=res)
+        f = K.linear(pc1, x, out_layout=K.OUT_GEGLU, ln=(rs, 1e-5))
+        return K.linear(pc2, f, residual=res)
+    return run, 2.0 * rows * 3 * Fh * C, None
+
+
 def gn_case(B, HW, C, stats):
     x = torch.randn(B, HW, C, device=DEV).to(BF)
     if stats:
@@ -156,6 +180,8 @@ CASES = {
     "conv3_l1_in_320": lambda: conv_case(8, 32, 32, 320, 640, temb=True, stats=True),
     "conv3_l1_res_640": lambda: conv_case(8, 32, 32, 640, 640, residual=True, stats=True),
     "conv3_l2_in_640": lambda: conv_case(8, 16, 16, 640, 1280, temb=True, stats=True),
+    "ff_l0": lambda: ff_case(8 * 4096),
+    "ff_l0_unfused": lambda: ff_case(8 * 4096, fused=False),
     "mm_8192": lambda: mm_case(8192, 8192, 8192),
     "mm_4096": lambda: mm_case(4096, 4096, 4096),
     "mm_geglu_320": lambda: mm_case(32768, 320, 2560),

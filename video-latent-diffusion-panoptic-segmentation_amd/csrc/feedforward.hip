@@ -1,0 +1,328 @@
+// Fused transformer feed-forward: diffusers FeedForward(GEGLU) of the 64x64 UNet level
+// (BasicTransformerBlock ff: ff.net.0 = GEGLU(C -> 2F), ff.net.2 = Linear(F -> C), + residual;
+// reached via /root/reference/ldmseg/models/unet.py:361-425) in ONE kernel whose GEGLU
+// intermediate never leaves the CU.
+//
+// Why: at C = 320, F = 1280, M = 32768 rows the unfused pair writes and re-reads an 84 MB
+// [M][F] intermediate and runs as two launches (the A-register-stationary GEGLU ~95 us, the
+// K = 1280 FF2 ~50 us; profiles/r03a_shape_breakdown.txt).  Here one 8-wave block per CU owns a
+// 128-row tile for both GEMMs:
+//   - the tile's rows x (the residual stream, LayerNorm norm3 folded as in ldm_conv2d's ln_rows
+//     form) sit in VGPRs as MFMA fragments for the whole tile (16 rows x 320 K per wave);
+//   - the hidden dimension is walked in 64-wide chunks: per chunk the 128 packed GEGLU columns
+//     (64 hidden + 64 gate, 16-column interleave) are computed from 5 LDS stages of W1 (128 x 64),
+//     h * gelu(g) is rounded to bf16 into a 16 KB LDS tile, and the FF2 accumulators (128 x 320
+//     fp32 in VGPRs) take that tile times one 320 x 64 stage of W2;
+//   - the weights stream by LDS-DMA through one chunk's worth of fixed stage regions (120 KB): a
+//     stage is re-filled for the next chunk as soon as it is consumed, so five stages are in
+//     flight (counted vmcnt, one raw barrier per stage); every CU streams the same weights, so
+//     they come from its XCD's L2.
+// Per chunk and tile: 15.7 MFLOP against 120 KB of weight stages (131 FLOP/B).
+// Epilogue: bf16(acc + b2) staged once, then ldm_conv2d's PRE row writer (residual, row
+// statistics) — the same rounding points and K order as the unfused ars GEGLU + tile FF2 pair
+// (per output element the same MFMA instruction sequence), so the results agree bit for bit.
+// Geometry: 512 threads = 8 waves.  GEGLU: 8 (M) x 1 (N), wave tile 16 rows x 128 packed columns
+// (8 fragments; each wave holds only its own rows of x); FF2: 4 (M) x 2 (N), wave tile 32 rows x
+// 160 columns (2 x 10 fragments: each W2 fragment read from LDS feeds two MFMAs); all
+// v_mfma_f32_16x16x32_bf16 with D[n][m] = W . X^T (lane (g, lr): channels 4g..4g+3 of row lr).
+#include "igemm_common.h"
+
+namespace {
+namespace ffk {
+constexpr int NT = 512;
+constexpr int BM = 128;                 // rows per tile
+constexpr int C = 320;                  // model width: GEGLU K and FF2 N
+constexpr int KC = C / 32;              // k32 fragments of a row of x (10)
+constexpr int CH = 64;                  // hidden channels per chunk
+constexpr int PW1 = 2 * CH;             // packed GEGLU columns per chunk (128)
+constexpr int KS1 = C / 64;             // W1 stages per chunk (5)
+constexpr int SPC = KS1 + 1;            // stages per chunk (5 x W1, 1 x W2)
+constexpr int FM = 2;                   // FF2: 16-row fragments per wave (32 rows)
+constexpr int FN1 = PW1 / 16;           // GEGLU: fragments per wave (all 128 packed columns: 8)
+constexpr int FN2 = C / 2 / 16;         // FF2 fragments per wave (160 columns: 10)
+constexpr int W1_B = PW1 * 128;         // a W1 stage: 128 packed rows x 64 K (16 KB)
+constexpr int W2_B = C * 128;           // the W2 stage: 320 rows x 64 K (40 KB)
+constexpr int W1_INS = PW1 / 8 / 8;     // DMA instructions per wave for a W1 stage (2)
+constexpr int W2_INS = C / 8 / 8;       // ... for the W2 stage (5)
+constexpr int CHUNK_INS = KS1 * W1_INS + W2_INS;
+// a chunk's six stages have fixed LDS regions (the ring holds exactly one chunk): W1 stage st at
+// st x 16 KB, W2 at 80 KB.  Stage (c + 1, st) is issued as soon as (c, st) is consumed, so five
+// stages (~100 KB) are in flight while one is multiplied.
+constexpr int H_OFF = KS1 * W1_B + W2_B;   // bf16 [128][64] GEGLU output tile (16 KB)
+__host__ __device__ constexpr int stage_ins(int st) { return st < KS1 ? W1_INS : W2_INS; }
+// DMA instructions a wave may leave in flight when it waits for stage st: every other stage of the
+// stream except st - 1 (just consumed, re-issued after the barrier); in the last chunk only the
+// stages after st (and (c, 5) is issued after the st = 0 wait)
+__host__ __device__ constexpr int younger_steady(int st) {
+  return CHUNK_INS - stage_ins(st) - stage_ins((st + SPC - 1) % SPC);
+}
+__host__ __device__ constexpr int younger_last(int st) {
+  int n = 0;
+  for (int s = st + 1; s < SPC; ++s) n += (st == 0 && s == SPC - 1) ? 0 : stage_ins(s);
+  return n;
+}
+constexpr int COL_OFF = H_OFF + BM * 128;
+constexpr int MAXF = 1280;              // hidden width bound: b1 and c1 ([2F] fp32 each) in LDS
+constexpr int LDS_B = COL_OFF + 2 * (2 * MAXF) * 4;
+constexpr int HP = C + 8;               // epilogue staging pitch (bf16)
+static_assert(BM * HP * 2 + BM * (C / 8) * 2 * 4 <= COL_OFF, "epilogue staging exceeds the ring + H");
+static_assert(LDS_B <= 160 * 1024, "LDS");
+}  // namespace ffk
+
+// s_waitcnt vmcnt(n) for the constant n of an unrolled stage (immediate operand)
+__device__ __forceinline__ void vm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+    case 7: asm volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+    case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 11: asm volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+static_assert(ffk::younger_steady(0) == 8 && ffk::younger_steady(1) == 11 && ffk::younger_steady(5) == 8 &&
+              ffk::younger_last(0) == 8 && ffk::younger_last(2) == 9 && ffk::younger_last(4) == 5 &&
+              ffk::younger_last(5) == 0, "vm_wait cases");
+
+__global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, const ConvArgs p2) {
+  using namespace ffk;
+  __shared__ uint4 smem[LDS_B / 16];
+  const int F = p2.kpad;                  // hidden width (FF2 K)
+  const int NC = F / CH;                  // chunks
+  const int M = g1.M;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 15, g = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int drow = lane >> 3;
+  const int dchunk = (lane & 7) ^ (((8 * wv + drow) >> 1) & 7);   // source-side swizzle (igemm)
+
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc((void*)g1.a0, 0, g1.a0_bytes, kBufFlags);
+  const __amdgpu_buffer_rsrc_t rw1 = __builtin_amdgcn_make_buffer_rsrc((void*)g1.w, 0, g1.w_bytes, kBufFlags);
+  const __amdgpu_buffer_rsrc_t rw2 = __builtin_amdgcn_make_buffer_rsrc((void*)p2.w, 0, p2.w_bytes, kBufFlags);
+  bf16_t* const hs = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(smem) + H_OFF);
+  float* const sb1 = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + COL_OFF);
+  float* const sc1 = sb1 + 2 * MAXF;
+
+  // the GEGLU column constants (packed bias, LayerNorm-fold column sums) once per block: a global
+  // load inside the stage loop would make hipcc drain the weight stream (vmcnt(0)) before its use
+  for (int i = tid; i < g1.n; i += NT) {
+    sb1[i] = g1.bias ? g1.bias[i] : 0.f;
+    sc1[i] = g1.ln_rows ? g1.ln_c1[i] : 0.f;
+  }
+
+  // stage st of chunk c: W1 K stage st (< 5) or the W2 stage (5), into its fixed LDS region
+  auto issue = [&](int c, int st) {
+#ifdef LDM_ABL_NO_LOADS   // ablation build: weights never fetched (LDS holds stale data)
+    return;
+#endif
+    const unsigned base = lds0 + (unsigned)(st * W1_B);
+    if (st < KS1) {
+#pragma unroll
+      for (int i = 0; i < W1_INS; ++i) {
+        const int qq = wv + 8 * i, r = 8 * qq + drow;
+        dma16(rw1, ((PW1 * c + r) * g1.kpad + 64 * st + 8 * dchunk) * 2, __builtin_amdgcn_readfirstlane(base + qq * 1024));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < W2_INS; ++i) {
+        const int qq = wv + 8 * i, n = 8 * qq + drow;
+        dma16(rw2, (n * F + CH * c + 8 * dchunk) * 2, __builtin_amdgcn_readfirstlane(base + qq * 1024));
+      }
+    }
+  };
+
+  const int tiles = (M + BM - 1) / BM;
+  for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const int m0 = tile * BM;
+    // ---- GEGLU rows of this wave: 16 wave + lr; x fragments: lane (g, lr) holds
+    //      x[row][32 kc + 8 g, +8) (40 VGPRs: the GEGLU runs 8 (M) x 1 (N) so no row is held twice)
+    const int mg = m0 + 16 * wave + lr;
+    uint4 xf[KC];
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) xf[kc] = bload(rx, mg < M ? (mg * C + 32 * kc + 8 * g) * 2 : kOOB);
+    const float2 lnr = (g1.ln_rows && mg < M) ? ln_row(g1, mg) : make_float2(1.f, 0.f);
+    f32x4_t acc2[FM][FN2];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN2; ++j) acc2[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    f32x4_t acc1[FN1];
+
+#pragma unroll
+    for (int st = 0; st < KS1; ++st) issue(0, st);
+    for (int c = 0; c < NC; ++c) {
+      const bool last = c + 1 == NC;
+#pragma unroll
+      for (int st = 0; st < SPC; ++st) {          // compile-time stage: x fragments by constant index
+        // stage (c, st) landed for this wave, then every wave's part (and (c, st - 1) is consumed)
+        vm_wait(last ? younger_last(st) : younger_steady(st));
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (st == 0) issue(c, SPC - 1);
+        else if (!last) issue(c + 1, st - 1);
+        const uint4* Ws = smem + st * (W1_B / 16);
+        if (st < KS1) {
+          if (st == 0) {
+#pragma unroll
+            for (int j = 0; j < FN1; ++j) acc1[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+          }
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+            for (int j = 0; j < FN1; ++j) {
+              const int r = 16 * j + lr;
+              Frag8<bf16_t> wf, xa;
+              wf.v = Ws[r * 8 + swz(r, 4 * ks + g)];
+              xa.v = xf[2 * st + ks];
+#ifdef LDM_ABL_NO_MFMA   // ablation build: fragments read, no MFMA issued
+              asm volatile("" ::"v"(wf.v.x), "v"(wf.v.w), "v"(xa.v.x));
+              continue;
+#endif
+              mma_k32(acc1[j], wf, xa);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          if (st == KS1 - 1) {
+            // h * gelu(g) (LayerNorm fold: rstd (acc - mean c1) + bias) -> bf16 H tile; fragments j
+            // (hidden) and j + 1 (gate) hold the same 4 channels of the same row in one lane
+#pragma unroll
+            for (int j = 0; j < FN1; j += 2) {
+              const int pc = PW1 * c + 16 * j + 4 * g;   // packed column
+              const int hl = 8 * j + 4 * g;              // hidden column in the chunk
+              const float4 bh = *reinterpret_cast<const float4*>(sb1 + pc);
+              const float4 bg = *reinterpret_cast<const float4*>(sb1 + pc + 16);
+              const float4 ch = *reinterpret_cast<const float4*>(sc1 + pc);
+              const float4 cg = *reinterpret_cast<const float4*>(sc1 + pc + 16);
+              const float bhv[4] = {bh.x, bh.y, bh.z, bh.w}, bgv[4] = {bg.x, bg.y, bg.z, bg.w};
+              const float chv[4] = {ch.x, ch.y, ch.z, ch.w}, cgv[4] = {cg.x, cg.y, cg.z, cg.w};
+              const int ml = 16 * wave + lr;
+              bf16_t h[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+#ifdef LDM_ABL_NO_GELU   // ablation build: the GEGLU epilogue's math replaced by one multiply-add
+                h[k] = f2bf(acc1[j][k] * acc1[j + 1][k] + bhv[k] + cgv[k]);
+#else
+                h[k] = f2bf(fmaf(lnr.y, chv[k], fmaf(lnr.x, acc1[j][k], bhv[k])) *
+                            gelu_f(fmaf(lnr.y, cgv[k], fmaf(lnr.x, acc1[j + 1][k], bgv[k]))));
+#endif
+              }
+              *reinterpret_cast<uint2*>(hs + ml * 64 + swz(ml, hl >> 3) * 8 + (hl & 7)) =
+                  *reinterpret_cast<const uint2*>(h);
+            }
+          }
+        } else {
+          // FF2: acc2 += H (128 x 64) . W2[:, 64 c, +64)^T
+          const uint4* Hs = reinterpret_cast<const uint4*>(hs);
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            Frag8<bf16_t> ha[FM];
+#pragma unroll
+            for (int i = 0; i < FM; ++i) {
+              const int ml = 32 * wm + 16 * i + lr;
+              ha[i].v = Hs[ml * 8 + swz(ml, 4 * ks + g)];
+            }
+#pragma unroll
+            for (int j = 0; j < FN2; ++j) {
+              const int r = 160 * wn + 16 * j + lr;
+              Frag8<bf16_t> wf;
+              wf.v = Ws[r * 8 + swz(r, 4 * ks + g)];
+#ifdef LDM_ABL_NO_MFMA
+              asm volatile("" ::"v"(wf.v.x), "v"(wf.v.w), "v"(ha[0].v.x), "v"(ha[1].v.y));
+              continue;
+#endif
+#pragma unroll
+              for (int i = 0; i < FM; ++i) mma_k32(acc2[i][j], wf, ha[i]);
+            }
+            // keep the next k32 step's fragment reads from being hoisted beside this step's
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+
+    // ---- epilogue: bf16(acc + b2) staged over the ring, then the PRE row writer (residual, row
+    //      statistics, 16-B row stores)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every wave left the ring / H
+    bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+    for (int j = 0; j < FN2; ++j) {
+      const int n = 160 * wn + 16 * j + 4 * g;
+      const float4 b4 = p2.bias ? *reinterpret_cast<const float4*>(p2.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ml = 32 * wm + 16 * i + lr;
+        bf16_t h[4] = {f2bf(acc2[i][j][0] + b4.x), f2bf(acc2[i][j][1] + b4.y), f2bf(acc2[i][j][2] + b4.z),
+                       f2bf(acc2[i][j][3] + b4.w)};
+        *reinterpret_cast<uint2*>(stg + ml * HP + n) = *reinterpret_cast<const uint2*>(h);
+      }
+    }
+    __syncthreads();
+    epilogue_fast<BM, C, NT, true>(p2, m0, 0, stg, HP, reinterpret_cast<float*>(smem) + BM * HP / 2);
+    __syncthreads();   // the next tile's x loads / stages reuse LDS
+  }
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// host side
+extern "C" int ldm_feedforward(const ldm_conv_params* g, const ldm_conv_params* f, ldm_stream_t stream) {
+  using namespace ffk;
+  if (!g || !f) return LDM_ERR_ARG;
+  const auto a16 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; };
+  const int64_t M = (int64_t)g->batch * g->h_out * g->w_out;
+  const int F = f->kpad;
+  if (g->dtype != LDM_BF16 || f->dtype != LDM_BF16 || g->ksize != 1 || f->ksize != 1 || g->stride != 1 ||
+      f->stride != 1 || g->upsample || f->upsample || g->a1 || g->c1 || f->c1)
+    return LDM_ERR_ARG;
+  if (g->c0 != C || g->kpad != C || f->n != C || g->out_layout != LDM_OUT_GEGLU || f->out_layout != LDM_OUT_NHWC)
+    return LDM_ERR_ARG;
+  if (F % CH || F > MAXF || g->n != 2 * F || f->c0 != F) return LDM_ERR_ARG;
+  if ((int64_t)f->batch * f->h_out * f->w_out != M || g->h_out != g->h_in || g->w_out != g->w_in) return LDM_ERR_ARG;
+  if (g->act != LDM_ACT_NONE || f->act != LDM_ACT_NONE || g->temb || f->temb || g->residual || g->row_stats ||
+      g->gn_partial || f->gn_partial || f->ln_rows || g->out_f32 || f->out_f32)
+    return LDM_ERR_ARG;
+  if (g->ln_rows && !g->ln_c1) return LDM_ERR_ARG;
+  if (!g->a0 || !g->w || !f->w || !f->out) return LDM_ERR_ARG;
+  if (!a16(g->a0) || !a16(g->w) || !a16(f->w) || !a16(f->out) || !a16(f->residual) || !a16(f->bias) ||
+      !a16(f->row_stats) || (g->ln_rows && !a16(g->ln_rows)))
+    return LDM_ERR_ALIGN;
+  if (M <= 0) return LDM_OK;
+  if (M * C * 2 >= (1LL << 31) - 64 || M * 16 >= (1LL << 31)) return LDM_ERR_ARG;
+
+  ConvArgs a1{}, a2{};
+  a1.a0 = (const char*)g->a0;
+  a1.a0_bytes = (int)(M * C * 2);
+  a1.c0 = C;
+  a1.w = (const char*)g->w;
+  a1.w_bytes = (int)((int64_t)g->n * g->kpad * 2);
+  a1.n = g->n;
+  a1.kpad = g->kpad;
+  a1.bias = g->bias;
+  a1.ln_rows = g->ln_rows;
+  a1.ln_c1 = g->ln_c1;
+  a1.ln_inv_k = g->ln_inv_k;
+  a1.ln_eps = g->ln_eps;
+  a1.M = (int)M;
+  a2.w = (const char*)f->w;
+  a2.w_bytes = (int)((int64_t)C * F * 2);
+  a2.n = C;
+  a2.kpad = F;
+  a2.bias = f->bias;
+  a2.residual = (const char*)f->residual;
+  a2.out = (char*)f->out;
+  a2.out_layout = LDM_OUT_NHWC;
+  a2.act = LDM_ACT_NONE;
+  a2.row_stats = f->row_stats;
+  a2.M = (int)M;
+  a2.hw_out = (int)M;
+  a2.ksplit = 1;
+  const int tiles = (int)((M + BM - 1) / BM);
+  const int grid = tiles < 256 ? tiles : 256;
+  hipLaunchKernelGGL(feedforward_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, a1, a2);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}

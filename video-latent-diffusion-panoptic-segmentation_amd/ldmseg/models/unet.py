@@ -527,6 +527,16 @@ class UNet(nn.Module):
         self._ln_fold = bool(enabled)
         self._plan = self._plan_key = self._dplan = None
 
+    @property
+    def ff_fused(self):
+        return getattr(self, "_ff_fused", True)
+
+    def set_ff_fused(self, enabled=True):
+        """bf16 inference with the LayerNorm fold: run the 64x64 level's FeedForward as one
+        ldm_feedforward launch (default on; K.feedforward_ok decides per call); off runs the GEGLU
+        and ff.net.2 GEMMs separately (A/B — the results are the same bit for bit)."""
+        self._ff_fused = bool(enabled)
+
     def _transformer(self, P, t, x, B, H, W, ehs):
         p = P[id(t)]
         C = x.shape[-1]
@@ -559,6 +569,10 @@ class UNet(nn.Module):
             L = e.shape[1]
             a = K.attention(q, kv, kv[..., C:], B, heads, dh, N, L, C, 2 * C, 2 * C)
             h = K.linear(q2["out"], a, residual=h, out=h)
+        if rs3 is not None and self.ff_fused and K.feedforward_ok(p["ff1_ln"], p["ff2"], h):
+            # ff.net.2(GEGLU(ff.net.0(norm3(h)))) + h in one launch, the 4C intermediate on chip
+            h = K.feedforward(p["ff1_ln"], p["ff2"], h, ln=(rs3, p["ln_eps"][1]), residual=h, out=h)
+            return K.conv2d(p["proj_out"], h, B, H, W, residual=x, gn_stats=True)
         if rs3 is not None:
             f = K.linear(p["ff1_ln"], h, out_layout=K.OUT_GEGLU, ln=(rs3, p["ln_eps"][1]))   # ff.net.0(norm3(h))
         else:

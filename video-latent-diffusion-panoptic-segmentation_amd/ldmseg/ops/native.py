@@ -70,6 +70,7 @@ EXPORTS = {
     "ldm_conv2d_set_wide": (None, [_i]),
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
+    "ldm_feedforward": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp, _i64, _vp]),
     "ldm_attention_fp8_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
@@ -642,6 +643,71 @@ def linear(pc: PackedConv, x, **kw):
         v = y.view(*x.shape[:-1], y.shape[-1])
     setattr(v, GN_PART_ATTR, gn_stats_of(y))
     return v
+
+
+FF_WIDTH = 320             # ldm_feedforward's model width (the 64x64 UNet level)
+FF_MIN_TILES = 256         # 128-row tiles below which the fused kernel leaves CUs idle (one per CU)
+
+
+def feedforward_ok(pc1: PackedConv, pc2: PackedConv, x):
+    """Whether ldm_feedforward takes this FeedForward: bf16, width 320, hidden F % 64 == 0 and
+    <= 1280, and enough rows for one 128-row tile per CU (fewer run the two-launch form)."""
+    rows = x.numel() // x.shape[-1]
+    F = pc2.kpad
+    return (x.dtype == torch.bfloat16 and pc1.dtype == torch.bfloat16 and pc2.dtype == torch.bfloat16
+            and x.shape[-1] == FF_WIDTH and pc1.geglu and pc1.ksize == 1 and pc2.ksize == 1 and pc1.kpad == FF_WIDTH
+            and pc2.n == FF_WIDTH and pc1.n == 2 * F and pc2.cin == F and F % 64 == 0 and F <= 1280
+            and -(-rows // 128) >= FF_MIN_TILES)
+
+
+def feedforward(pc1: PackedConv, pc2: PackedConv, x, *, ln=None, residual=None, out=None, row_stats=None):
+    """FeedForward(GEGLU) in one launch (ldm_feedforward): out = Linear2(h * gelu(g)) (+ residual)
+    with [h | g] = Linear1(x) (LayerNorm-folded when ln = (rows, eps) and pc1 is a packed_ln_fold
+    weight).  Equal bit for bit to linear(pc2, linear(pc1, x, out_layout=OUT_GEGLU, ln=ln),
+    residual=residual, out=out, row_stats=row_stats); x [..., 320]."""
+    lib = load_library()
+    _gpu(x, pc1.w, pc2.w, residual, out, row_stats)
+    _contig(x, "x")
+    _contig(residual, "residual")
+    rows = x.numel() // x.shape[-1]
+    C, F = x.shape[-1], pc2.kpad
+    if not (pc1.geglu and pc1.n == 2 * F and pc1.kpad == C and pc2.n == C and pc2.cin == F):
+        raise ValueError("feedforward: pc1 must be the GEGLU pack [2F][C] and pc2 the [C][F] pack")
+    if x.dtype != pc1.dtype:
+        raise TypeError("feedforward: x dtype != packed weight dtype")
+    if out is None:
+        out = torch.empty(x.shape[:-1] + (C,), dtype=x.dtype, device=x.device)
+    elif out.numel() != rows * C or out.dtype != x.dtype or not out.is_contiguous():
+        raise ValueError("feedforward: preallocated out has the wrong size / dtype / layout")
+    if residual is not None and (residual.numel() != rows * C or residual.dtype != x.dtype):
+        raise ValueError("feedforward: residual must match the output")
+    if row_stats is not None and (row_stats.dtype != torch.float64 or row_stats.numel() != 2 * rows
+                                  or not row_stats.is_contiguous()):
+        raise ValueError("row_stats must be a contiguous fp64 [M, 2] tensor")
+    ln_rows, ln_c1, inv_k, eps = None, None, 0.0, 0.0
+    if ln is not None:
+        ln_rows, eps = ln
+        if getattr(pc1, "ln_c1", None) is None:
+            raise ValueError("ln needs a packed_ln_fold weight")
+        if ln_rows.dtype != torch.float64 or ln_rows.numel() != 2 * rows or not ln_rows.is_contiguous():
+            raise ValueError("ln rows must be a contiguous fp64 [M, 2] tensor")
+        ln_c1, inv_k = pc1.ln_c1, 1.0 / C
+    dt = dtype_code(x.dtype)
+    g = ConvParams(_ptr(x), None, C, 0, rows, 1, 1, 1, 1, 1, 1, 0, _ptr(pc1.w), pc1.n, pc1.kpad, _ptr(pc1.bias),
+                   None, 0, None, None, OUT_GEGLU, ACT_NONE, dt, 0, None, 0, None, 0, 0, 0, None, _ptr(ln_rows),
+                   _ptr(ln_c1), float(inv_k), float(eps))
+    f = ConvParams(None, None, F, 0, rows, 1, 1, 1, 1, 1, 1, 0, _ptr(pc2.w), C, F, _ptr(pc2.bias), None, 0,
+                   _ptr(residual), _ptr(out), OUT_NHWC, ACT_NONE, dt, 0, None, 0, None, 0, 0, 0, _ptr(row_stats),
+                   None, None, 0.0, 0.0)
+    ev = _prof_start()
+    _check(lib.ldm_feedforward(ctypes.byref(g), ctypes.byref(f), _stream(x)), "ldm_feedforward")
+    setattr(out, GN_PART_ATTR, None)
+    if ev is not None:
+        flops = 2.0 * rows * (2 * F * C + C * F)
+        nbytes = (x.numel() + out.numel() + (0 if residual is None else residual.numel())) * x.element_size() + \
+            (pc1.w.numel() + pc2.w.numel()) * pc1.w.element_size()
+        _prof_stop(ev, "igemm", flops, nbytes, f"ff M={rows} C={C} F={F}")
+    return out
 
 
 # ======================================================================================
