@@ -18,6 +18,16 @@
 //     flight (counted vmcnt, one raw barrier per stage); every CU streams the same weights, so
 //     they come from its XCD's L2.
 // Per chunk and tile: 15.7 MFLOP against 120 KB of weight stages (131 FLOP/B).
+// Measured (tools/opbench.py ff_l0, M = 32768): 110 us against 136-140 us for the two launches;
+// ablations: no weight loads 87 us, no GELU math 91 us — the GELU VALU (16 values per lane and
+// chunk, all waves in the same phase) and the weight stream each still cost ~20 us over the
+// ~32 us of MFMA work.  What it took (each step measured): the x rows' compiler-visible wait
+// before the stage loop (without it hipcc put vmcnt(n) waits for them inside the loop, draining
+// the weight stream every stage), DMA source offsets split into one lane VGPR + soffset, an
+// opaque thread index for the row writer (its hoisted address arithmetic held ~100 VGPRs through
+// the loop), and sched_group_barrier windows that keep LDS reads two fragments ahead of the
+// MFMAs (the default schedule reused one register quad).  Packed-f32 GELU (v_pk_fma) and a
+// 4-wave / 512-register form were measured slower (114, 160 us).
 // Epilogue: bf16(acc + b2) staged once, then ldm_conv2d's PRE row writer (residual, row
 // statistics) — the same rounding points and K order as the unfused ars GEGLU + tile FF2 pair
 // (per output element the same MFMA instruction sequence), so the results agree bit for bit.
@@ -63,7 +73,7 @@ __host__ __device__ constexpr int younger_last(int st) {
 }
 constexpr int COL_OFF = H_OFF + BM * 128;
 constexpr int MAXF = 1280;              // hidden width bound: b1 and c1 ([2F] fp32 each) in LDS
-constexpr int LDS_B = COL_OFF + 2 * (2 * MAXF) * 4;
+constexpr int LDS_B = COL_OFF + 2 * (2 * MAXF) * 4 + C * 4;   // + b2
 constexpr int HP = C + 8;               // epilogue staging pitch (bf16)
 static_assert(BM * HP * 2 + BM * (C / 8) * 2 * 4 <= COL_OFF, "epilogue staging exceeds the ring + H");
 static_assert(LDS_B <= 160 * 1024, "LDS");
@@ -107,6 +117,7 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
   bf16_t* const hs = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(smem) + H_OFF);
   float* const sb1 = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + COL_OFF);
   float* const sc1 = sb1 + 2 * MAXF;
+  float* const sb2 = sc1 + 2 * MAXF;
 
   // the GEGLU column constants (packed bias, LayerNorm-fold column sums) once per block: a global
   // load inside the stage loop would make hipcc drain the weight stream (vmcnt(0)) before its use
@@ -114,24 +125,30 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
     sb1[i] = g1.bias ? g1.bias[i] : 0.f;
     sc1[i] = g1.ln_rows ? g1.ln_c1[i] : 0.f;
   }
+  for (int i = tid; i < C; i += NT) sb2[i] = p2.bias ? p2.bias[i] : 0.f;
 
+  const int vo1 = (drow * g1.kpad + 8 * dchunk) * 2, vo2 = (drow * F + 8 * dchunk) * 2;
   // stage st of chunk c: W1 K stage st (< 5) or the W2 stage (5), into its fixed LDS region
   auto issue = [&](int c, int st) {
 #ifdef LDM_ABL_NO_LOADS   // ablation build: weights never fetched (LDS holds stale data)
     return;
 #endif
     const unsigned base = lds0 + (unsigned)(st * W1_B);
+    // lane part of the source offset (row drow of a DMA instruction's 8, swizzled chunk) in one
+    // loop-invariant VGPR, the instruction's rows / K stage / chunk in soffset
     if (st < KS1) {
 #pragma unroll
       for (int i = 0; i < W1_INS; ++i) {
-        const int qq = wv + 8 * i, r = 8 * qq + drow;
-        dma16(rw1, ((PW1 * c + r) * g1.kpad + 64 * st + 8 * dchunk) * 2, __builtin_amdgcn_readfirstlane(base + qq * 1024));
+        const int qq = wv + 8 * i;
+        dma16s(rw1, vo1, __builtin_amdgcn_readfirstlane(((PW1 * c + 8 * qq) * g1.kpad + 64 * st) * 2),
+               __builtin_amdgcn_readfirstlane(base + qq * 1024));
       }
     } else {
 #pragma unroll
       for (int i = 0; i < W2_INS; ++i) {
-        const int qq = wv + 8 * i, n = 8 * qq + drow;
-        dma16(rw2, (n * F + CH * c + 8 * dchunk) * 2, __builtin_amdgcn_readfirstlane(base + qq * 1024));
+        const int qq = wv + 8 * i;
+        dma16s(rw2, vo2, __builtin_amdgcn_readfirstlane((8 * qq * F + CH * c) * 2),
+               __builtin_amdgcn_readfirstlane(base + qq * 1024));
       }
     }
   };
@@ -139,6 +156,9 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
   const int tiles = (M + BM - 1) / BM;
   for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int m0 = tile * BM;
+    // the first chunk's W1 stages fly while x and the LayerNorm rows load
+#pragma unroll
+    for (int st = 0; st < KS1; ++st) issue(0, st);
     // ---- GEGLU rows of this wave: 16 wave + lr; x fragments: lane (g, lr) holds
     //      x[row][32 kc + 8 g, +8) (40 VGPRs: the GEGLU runs 8 (M) x 1 (N) so no row is held twice)
     const int mg = m0 + 16 * wave + lr;
@@ -152,9 +172,10 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
 #pragma unroll
       for (int j = 0; j < FN2; ++j) acc2[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     f32x4_t acc1[FN1];
-
-#pragma unroll
-    for (int st = 0; st < KS1; ++st) issue(0, st);
+    // a wait hipcc can see: its waitcnt model does not count the asm LDS-DMA, so with x still
+    // "pending" it would put vmcnt(n) waits before the x fragments' uses inside the stage loop —
+    // draining the weight stream every stage.  One full wait per tile instead (vmcnt(0)).
+    __builtin_amdgcn_s_waitcnt(0x0f70);
     for (int c = 0; c < NC; ++c) {
       const bool last = c + 1 == NC;
 #pragma unroll
@@ -172,18 +193,30 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
           }
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
+            Frag8<bf16_t> wf[FN1], xa;        // all of the step's W fragments in flight at once
 #pragma unroll
             for (int j = 0; j < FN1; ++j) {
               const int r = 16 * j + lr;
-              Frag8<bf16_t> wf, xa;
-              wf.v = Ws[r * 8 + swz(r, 4 * ks + g)];
-              xa.v = xf[2 * st + ks];
+              wf[j].v = Ws[r * 8 + swz(r, 4 * ks + g)];
+            }
+            xa.v = xf[2 * st + ks];
+#pragma unroll
+            for (int j = 0; j < FN1; ++j) {
 #ifdef LDM_ABL_NO_MFMA   // ablation build: fragments read, no MFMA issued
-              asm volatile("" ::"v"(wf.v.x), "v"(wf.v.w), "v"(xa.v.x));
+              asm volatile("" ::"v"(wf[j].v.x), "v"(wf[j].v.w), "v"(xa.v.x));
               continue;
 #endif
-              mma_k32(acc1[j], wf, xa);
+              mma_k32(acc1[j], wf[j], xa);
             }
+            // a sliding window of LDS reads two fragments ahead of the MFMAs (the default schedule
+            // reuses one register quad: every MFMA then waits out its ds_read)
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+            for (int j = 0; j < FN1 - 2; ++j) {
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
             __builtin_amdgcn_sched_barrier(0);
           }
           if (st == KS1 - 1) {
@@ -237,6 +270,14 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
 #pragma unroll
               for (int i = 0; i < FM; ++i) mma_k32(acc2[i][j], wf, ha[i]);
             }
+            // H fragments and one W fragment ahead, then one W read per MFMA pair
+            __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+            for (int j = 0; j < FN2 - 1; ++j) {
+              __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+              __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
             // keep the next k32 step's fragment reads from being hoisted beside this step's
             __builtin_amdgcn_sched_barrier(0);
           }
@@ -251,7 +292,7 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
 #pragma unroll
     for (int j = 0; j < FN2; ++j) {
       const int n = 160 * wn + 16 * j + 4 * g;
-      const float4 b4 = p2.bias ? *reinterpret_cast<const float4*>(p2.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 b4 = *reinterpret_cast<const float4*>(sb2 + n);
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int ml = 32 * wm + 16 * i + lr;
@@ -261,7 +302,12 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
       }
     }
     __syncthreads();
-    epilogue_fast<BM, C, NT, true>(p2, m0, 0, stg, HP, reinterpret_cast<float*>(smem) + BM * HP / 2);
+    // the row writer sees an opaque copy of the thread index: otherwise its per-thread address
+    // arithmetic is hoisted above the stage loop and held in VGPRs through it, leaving no room to
+    // keep a step's W fragments in flight
+    int tid_late = tid;
+    asm volatile("" : "+v"(tid_late));
+    epilogue_fast<BM, C, NT, true>(p2, m0, 0, stg, HP, reinterpret_cast<float*>(smem) + BM * HP / 2, tid_late);
     __syncthreads();   // the next tile's x loads / stages reuse LDS
   }
 }

@@ -125,6 +125,21 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, int voff, uns
       : "memory");
 }
 
+// dma16 with a wave-uniform byte offset in soffset: the per-lane part of the address stays one
+// loop-invariant VGPR, so no per-instruction offsets are precomputed, held (or spilled) across a loop
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t rsrc, int voff, int soff, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds_addr)
+      : "memory");
+}
+
 // One byte per lane global -> LDS (M0 + lane): an L2 prefetch of the lane's line that needs no
 // destination VGPR (a register load would leave a late write the compiler does not know about).
 // Counted on vmcnt like the operand DMA; an out-of-range offset (kOOB) makes no memory access.
@@ -494,8 +509,8 @@ __device__ __forceinline__ bool fast_temb_ok(const ConvArgs& p, int m0, int rows
 // elements); only the residual, the stores and the GroupNorm statistics are left.
 template <int ROWS, int COLS, int NT, bool PRE = false>
 __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0, const void* stage_v, int pitch,
-                                              float* red) {
-  const int tid = threadIdx.x;
+                                              float* red, int tid_in = -1) {
+  const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x;
   const int N = p.n;
   const float* stage = reinterpret_cast<const float*>(stage_v);
   if (!PRE && p.out_layout == LDM_OUT_GEGLU) {
