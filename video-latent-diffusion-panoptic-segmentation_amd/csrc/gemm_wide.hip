@@ -111,6 +111,7 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
     m0 = tm * BM;
     n0 = tn * BN;
   };
+  const int vob = (drow * p.kpad + dchunk * 8) * 2;
   // step s of this block's stream = K tile (s mod nks) of its tile s / nks
   auto issue = [&](int s) {
 #ifdef LDM_ABL_NO_LOADS
@@ -134,12 +135,14 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
       if (sel) dma16(ra1, off, dst);
       else dma16(ra0, off, dst);
     }
+    // B rows are always in range (N is a multiple of the tile): the lane part of the offset stays
+    // one loop-invariant VGPR and the rows / K tile go in soffset (per-instruction offsets held in
+    // VGPRs spilled, and hipcc's waits for the reloads drained the DMA stream)
 #pragma unroll
     for (int i = 0; i < B_INS; ++i) {
       const int q = wv + 8 * i;
-      const int n = n0 + 8 * q + drow;
-      const int off = n < p.n ? (n * p.kpad + k0 + dchunk * 8) * 2 : kOOB;
-      dma16(rw, off, __builtin_amdgcn_readfirstlane(bbase + q * 8 * 128));
+      dma16s(rw, vob, __builtin_amdgcn_readfirstlane(((n0 + 8 * q) * p.kpad + k0) * 2),
+             __builtin_amdgcn_readfirstlane(bbase + q * 8 * 128));
     }
     if (kt == 1) {
       // instruction wv: 0, 1 bias [256 wv, +256); 2, 3 c1; 4..7 fp64 rows [m0 + 64 (wv - 4), +64)
@@ -191,21 +194,22 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
 
   f32x4_t acc[FM][FN];
   auto compute = [&](int slot) {
-    const uint4* As = smem + slot * SLOT_U4;
-    const uint4* Bs = As + BM * 8;
+    // row r = base + 16 f + lr: swz(r, c) = c ^ ((lr >> 1) & 7) for every fragment f, so each
+    // operand needs one lane address per k32 step and the fragments are immediate offsets (the
+    // per-fragment addresses otherwise occupied ~10 VGPRs that spilled)
+    const uint4* As = smem + slot * SLOT_U4 + (wm * WM + lr) * 8;
+    const uint4* Bs = smem + slot * SLOT_U4 + BM * 8 + (wn * WN + lr) * 8;
+    const int sl = (lr >> 1) & 7;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      const int cch = (ks * 4 + g) ^ sl;
       Frag8<bf16_t> af[FM];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int r = wm * WM + i * 16 + lr;
-        af[i].v = As[r * 8 + swz(r, ks * 4 + g)];
-      }
+      for (int i = 0; i < FM; ++i) af[i].v = As[i * 128 + cch];
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        const int r = wn * WN + j * 16 + lr;
         Frag8<bf16_t> bf;
-        bf.v = Bs[r * 8 + swz(r, ks * 4 + g)];
+        bf.v = Bs[j * 128 + cch];
 #ifdef LDM_ABL_NO_MFMA   // ablation build: fragments read from LDS, no MFMA issued
         asm volatile("" ::"v"(bf.v.x), "v"(bf.v.w));
         if (j == 0) {
