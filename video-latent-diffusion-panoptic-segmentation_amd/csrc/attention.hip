@@ -690,6 +690,43 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
       glds16(vs, vb + off);
     }
   };
+  // full tiles: every lane's source is fixed but for the tile's key offset, so each of a wave's
+  // (at most two) K/V chunk slots keeps a pointer that advances by one tile of rows per issue
+  // (lanes of the constant columns 40..71 point at the ones / zeros rows and do not advance);
+  // the general form above (bounds, selects, 64-bit multiplies per tile) serves the first and the
+  // ragged last tile only
+  constexpr int NSL = (RCH * (KT / 64) + NW - 1) / NW;   // chunk slots per wave
+  const char* kq[NSL];
+  const char* vq[NSL];
+  int64_t kstep[NSL], vstep[NSL];
+#pragma unroll
+  for (int s2 = 0; s2 < NSL; ++s2) {
+    const int i = wave + NW * s2;
+    const int L = i * 64 + lane;
+    const int row = L / RCH, c = L - row * RCH;
+    const bool dat = i < RCH * (KT / 64) && c < CPR && c * EPC < p.d;
+    const bool one = c == ONES_CHUNK;
+    kq[s2] = dat ? reinterpret_cast<const char*>(kp + (int64_t)(KT + row) * p.ks + c * EPC)
+                 : reinterpret_cast<const char*>(one ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
+    vq[s2] = dat ? reinterpret_cast<const char*>(vp + (int64_t)(KT + row) * p.vs + c * EPC)
+                 : reinterpret_cast<const char*>(one ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
+    kstep[s2] = dat ? (int64_t)KT * p.ks * ES : 0;
+    vstep[s2] = dat ? (int64_t)KT * p.vs * ES : 0;
+  }
+  auto issue_full = [&](int buf) {   // the next full tile (tile 1, 2, ... in order)
+    const unsigned kb = lds0 + (unsigned)(buf * 2 * TILE * ES);
+    const unsigned vb = kb + TILE * ES;
+#pragma unroll
+    for (int s2 = 0; s2 < NSL; ++s2) {
+      const int i = wave + NW * s2;
+      if (i >= RCH * (KT / 64)) break;
+      const unsigned off = __builtin_amdgcn_readfirstlane(i * 64 * 16);
+      glds16(kq[s2], kb + off);
+      glds16(vq[s2], vb + off);
+      kq[s2] += kstep[s2];
+      vq[s2] += vstep[s2];
+    }
+  };
   const float c2 = p.scale_log2;
 
   // Q^T (B operand) chunk c: lane holds Q[q = qbase + r32][d = 16c + 8hh .. +8] * c2; the max
@@ -803,7 +840,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int t = 0; t < nfull; ++t) {
-    if (t + 1 < ntiles) issue_tile((t + 1) * KT, (t + 1) & 1);
+    if (t + 1 < nfull) issue_full((t + 1) & 1);
+    else if (t + 1 < ntiles) issue_tile((t + 1) * KT, (t + 1) & 1);
 #pragma unroll
     for (int hf = 0; hf < KT / 64; ++hf) compute(t & 1, t * KT, false, t == 0, hf);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
