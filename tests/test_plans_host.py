@@ -58,3 +58,18 @@ def test_describe_plan_rejects_what_conv2d_rejects():
     assert _p(batch=1, h=8, w=8, c0=12, n=64)["kind"] == "tile"     # c0 padded to 16: legal
     with pytest.raises(RuntimeError):
         _p(batch=1, h=8, w=8, c0=16, n=64, ksize=3, stride=2, upsample=True)   # upsample + stride 2
+
+
+def test_feedforward_fused_only_where_it_fills_the_chip():
+    """ldm_feedforward (one 128-row tile per CU) takes the 64x64 level's FeedForward at B >= 8
+    frames; a single frame (32 tiles) keeps the two-launch form."""
+    import torch
+    bf = torch.bfloat16
+    w1, w2 = torch.randn(2560, 320) * 0.05, torch.randn(320, 1280) * 0.03
+    pc1 = K.PackedConv(w1, torch.zeros(2560), bf, geglu=True)
+    pc2 = K.PackedConv(w2, torch.zeros(320), bf)
+    assert K.feedforward_ok(pc1, pc2, torch.empty(8, 4096, 320, dtype=bf))
+    assert not K.feedforward_ok(pc1, pc2, torch.empty(1, 4096, 320, dtype=bf))
+    assert not K.feedforward_ok(K.PackedConv(w1, None, bf), pc2, torch.empty(8, 4096, 320, dtype=bf))
+    with pytest.raises(RuntimeError):           # CPU tensors: no fallback path
+        K.feedforward(pc1, pc2, torch.empty(8, 4096, 320, dtype=bf))
