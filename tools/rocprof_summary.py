@@ -28,9 +28,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # (family, regex on the kernel name, is_primary) — primary kernels count calls
 FAMILIES = [
-    ("igemm", r"(igemm_kernel|igemm_big_kernel|conv3_halo_kernel|gemm_ars2?_kernel)<", True),
+    ("igemm", r"(igemm_kernel|igemm_big_kernel|conv3_halo_kernel|gemm_ars2?_kernel|gemm_wide_kernel)<|feedforward_kernel", True),
     ("igemm", r"splitk_epilogue_kernel<", False),
-    ("attention", r"attn(32|_d40)?_kernel<", True),
+    ("attention", r"attn(32|_d40|_f8)?_kernel<", True),
     ("group_norm", r"gn_apply", True),
     ("group_norm", r"gn_(partial|finalize)", False),
     ("layer_norm", r"ln_kernel<", True),
