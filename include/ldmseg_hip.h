@@ -159,8 +159,14 @@ void ldm_conv2d_set_epilogue(int mode);
  *          and out), out [M][320], optional row_stats; a0 ignored (the intermediate).
  * Scope: bf16, model width 320 (the 64x64 UNet level), F a multiple of 64 up to 1280; no time
  * embedding, activation, GroupNorm partials, split-K or fp32 output.  Results equal the two
- * separate calls bit for bit (same MFMA sequence per element, same bf16 rounding points). */
-int ldm_feedforward(const ldm_conv_params* geglu, const ldm_conv_params* ff2, ldm_stream_t stream);
+ * separate calls bit for bit (same MFMA sequence per element, same bf16 rounding points).
+ *   proj_out: optional (NULL = none) — Transformer2DModel.proj_out applied to the feed-forward's
+ *          output as a third 1x1 call (320 -> 320, bias, residual = the transformer input,
+ *          out, optional gn_partial / gn_unit / gn_slots; batch / h_out / w_out give the image
+ *          of each row for the GroupNorm partials).  The feed-forward's output h then never
+ *          reaches HBM: ff2's out may be NULL and its row_stats must be. */
+int ldm_feedforward(const ldm_conv_params* geglu, const ldm_conv_params* ff2, const ldm_conv_params* proj_out,
+                    ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).

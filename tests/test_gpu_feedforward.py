@@ -133,3 +133,35 @@ def test_unet_forward_fused_equals_unfused():
     torch.cuda.synchronize()
     assert torch.isfinite(y1.float()).all()
     assert torch.equal(y0, y1)
+
+
+@pytest.mark.parametrize("B,HW", [(8, 64), (3, 64)])
+def test_feedforward_with_proj_out_matches_three_launches(B, HW):
+    """ldm_feedforward with Transformer2DModel.proj_out behind it (h never stored) vs the fused
+    feed-forward followed by the separate proj_out conv (residual = transformer input, GroupNorm
+    partials): the same output bits; the GroupNorm totals per (image, unit) within the rounding of
+    their fp32 partials."""
+    M = B * HW * HW
+    w1, b1, w2, b2, gamma, beta = _weights(1280, 7)
+    g = torch.Generator().manual_seed(8)
+    wpo = (torch.randn(C, C, generator=g) * C ** -0.5).to(DEV)
+    bpo = (torch.randn(C, generator=g) * 0.1).to(DEV)
+    pc1 = K.packed_ln_fold(w1, b1, gamma, beta, BF, geglu=True)
+    pc2 = K.PackedConv(w2, b2, BF)
+    pc3 = K.PackedConv(wpo, bpo, BF)
+    h = (torch.randn(M, C, device=DEV) * 1.5 + 0.3).to(BF)
+    x_in = torch.randn(B, HW, HW, C, device=DEV).to(BF)
+    lnarg = (_row_stats(h), 1e-5)
+    ha = h.clone()
+    K.feedforward(pc1, pc2, ha, ln=lnarg, residual=ha, out=ha)
+    ya = K.conv2d(pc3, ha, B, HW, HW, residual=x_in, gn_stats=True)
+    hb = h.clone()
+    yb = K.feedforward(pc1, pc2, hb, ln=lnarg, residual=hb, proj_out=(pc3, x_in, B, HW, HW, True))
+    torch.cuda.synchronize()
+    assert torch.equal(ya.view(-1), yb.view(-1)), f"max |diff| {(ya.float() - yb.float()).abs().max().item()}"
+    assert torch.equal(hb, h)                      # the feed-forward's output was not stored
+    pa, pb = K.gn_stats_of(ya), K.gn_stats_of(yb)
+    assert pa is not None and pb is not None and pa.shape == pb.shape
+    # per (batch, unit) totals: the separate conv may plan other row tiles (B = 3: 64-row tiles),
+    # which spreads the partials over the slots and groups the fp32 sums differently
+    assert torch.allclose(pa.sum(1), pb.sum(1), rtol=1e-6, atol=1e-3)

@@ -90,7 +90,7 @@ def attn_bwd_case(B, N, C, heads=8, new=True):
     return run, 10.0 * B * heads * N * N * d, None     # five N x N x d matmuls (S, dP, dV, dK, dQ)
 
 
-def ff_case(rows, fused=True, Fh=1280):
+def ff_case(rows, fused=True, Fh=1280, proj_out=False):
     """The transformer FeedForward at width 320 (LayerNorm-folded GEGLU + ff.net.2 + residual): the
     fused ldm_feedforward or the two ldm_conv2d launches it replaces."""
     C = 320
@@ -106,7 +106,15 @@ def ff_case(rows, fused=True, Fh=1280):
     rs = torch.stack([xd.sum(-1), (xd * xd).sum(-1)], -1).reshape(-1).contiguous()
     res = torch.randn(rows, C, device=DEV).to(BF)
 
+    pc3 = K.PackedConv(torch.randn(C, C, device=DEV, generator=g) * 0.05, torch.randn(C, device=DEV), BF)
+    B, HW = rows // 4096, 64
+
     def run():
+        if proj_out:
+            if fused:
+                return K.feedforward(pc1, pc2, x, ln=(rs, 1e-5), residual=res, proj_out=(pc3, res, B, HW, HW, True))
+            h = K.feedforward(pc1, pc2, x, ln=(rs, 1e-5), residual=res)
+            return K.conv2d(pc3, h, B, HW, HW, residual=res, gn_stats=True)
         if fused:
             return K.feedforward(pc1, pc2, x, ln=(rs, 1e-5), residual=res)
         f = K.linear(pc1, x, out_layout=K.OUT_GEGLU, ln=(rs, 1e-5))
@@ -182,6 +190,8 @@ CASES = {
     "conv3_l2_in_640": lambda: conv_case(8, 16, 16, 640, 1280, temb=True, stats=True),
     "ff_l0": lambda: ff_case(8 * 4096),
     "ff_l0_unfused": lambda: ff_case(8 * 4096, fused=False),
+    "ff_po_l0": lambda: ff_case(8 * 4096, proj_out=True),
+    "ff_po_l0_separate": lambda: ff_case(8 * 4096, fused=False, proj_out=True),
     "mm_8192": lambda: mm_case(8192, 8192, 8192),
     "mm_4096": lambda: mm_case(4096, 4096, 4096),
     "mm_geglu_320": lambda: mm_case(32768, 320, 2560),

@@ -73,9 +73,14 @@ __host__ __device__ constexpr int younger_last(int st) {
 }
 constexpr int COL_OFF = H_OFF + BM * 128;
 constexpr int MAXF = 1280;              // hidden width bound: b1 and c1 ([2F] fp32 each) in LDS
-constexpr int LDS_B = COL_OFF + 2 * (2 * MAXF) * 4 + C * 4;   // + b2
+constexpr int COL_END = COL_OFF + 2 * (2 * MAXF) * 4 + C * 4;   // + b2
+// proj_out behind the feed-forward reuses all of it: five [128][64] h images (80 KB) + two
+// 320 x 64 weight slots (80 KB)
+constexpr int LDS_B = 160 * 1024;
+static_assert(COL_END <= LDS_B && KS1 * BM * 128 + 2 * C * 128 <= LDS_B, "LDS");
 constexpr int HP = C + 8;               // epilogue staging pitch (bf16)
 static_assert(BM * HP * 2 + BM * (C / 8) * 2 * 4 <= COL_OFF, "epilogue staging exceeds the ring + H");
+static_assert(BM * HP * 2 + gn_red_floats<NT, C, BM, 8>() * 4 <= LDS_B, "proj_out GroupNorm scratch exceeds LDS");
 static_assert(LDS_B <= 160 * 1024, "LDS");
 }  // namespace ffk
 
@@ -95,7 +100,128 @@ static_assert(ffk::younger_steady(0) == 8 && ffk::younger_steady(1) == 11 && ffk
               ffk::younger_last(0) == 8 && ffk::younger_last(2) == 9 && ffk::younger_last(4) == 5 &&
               ffk::younger_last(5) == 0, "vm_wait cases");
 
-__global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, const ConvArgs p2) {
+// Transformer2DModel.proj_out fused behind the feed-forward (ldm_feedforward with a third
+// parameter block): the feed-forward's output rows h = bf16(bf16(acc + b2) + h_old) go straight
+// into LDS as the A operand of proj_out (5 x [128 rows][64 K] swizzled images, 80 KB) instead of
+// to HBM, then out = proj_out(h) + x_in over five 320 x 64 weight stages (two 40 KB slots), with
+// ldm_conv2d's PRE row writer (residual, GroupNorm partials) — the same values and rounding
+// points as the separate proj_out call on the stored h.
+__device__ __forceinline__ void proj_out_tile(const ConvArgs& p2, const ConvArgs& p3, __amdgpu_buffer_rsrc_t rw3,
+                                              int m0, f32x4_t (&acc)[ffk::FM][ffk::FN2], uint4* smem,
+                                              unsigned lds0, int tid, int wv, int lane) {
+  using namespace ffk;
+  const int wave = tid >> 6, wm = wave >> 1, wn = wave & 1;
+  const int lr = lane & 15, g = lane >> 4;
+  const int drow = lane >> 3;
+  const int dchunk = (lane & 7) ^ (((8 * wv + drow) >> 1) & 7);
+  constexpr int HA_B = BM * 128;          // one [128][64] K image of h
+  constexpr int SL0 = 0;                  // the two weight slots, then the five h images
+  constexpr int HA0 = 2 * W2_B;
+  const int vo3 = (drow * C + 8 * dchunk) * 2;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every wave left the ring / H / columns
+  // h = bf16(bf16(acc + b2) + h_old) into the A images (lane: channels n..n+3 of row ml)
+  bf16_t* ha = reinterpret_cast<bf16_t*>(reinterpret_cast<char*>(smem) + HA0);
+  const bf16_t* hold = reinterpret_cast<const bf16_t*>(p2.residual);
+#pragma unroll
+  for (int j = 0; j < FN2; ++j) {
+    const int n = 160 * wn + 16 * j + 4 * g;
+    const float4 b4 = p2.bias ? *reinterpret_cast<const float4*>(p2.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ml = 32 * wm + 16 * i + lr;
+      const int m = m0 + ml;
+      float r[4] = {0.f, 0.f, 0.f, 0.f};
+      if (hold && m < p3.M) {
+        const uint2 u = *reinterpret_cast<const uint2*>(hold + (int64_t)m * C + n);
+        r[0] = __uint_as_float(u.x << 16); r[1] = __uint_as_float(u.x & 0xffff0000u);
+        r[2] = __uint_as_float(u.y << 16); r[3] = __uint_as_float(u.y & 0xffff0000u);
+      }
+      bf16_t h[4];
+      h[0] = f2bf(bf2f(f2bf(acc[i][j][0] + b4.x)) + r[0]);
+      h[1] = f2bf(bf2f(f2bf(acc[i][j][1] + b4.y)) + r[1]);
+      h[2] = f2bf(bf2f(f2bf(acc[i][j][2] + b4.z)) + r[2]);
+      h[3] = f2bf(bf2f(f2bf(acc[i][j][3] + b4.w)) + r[3]);
+      const int kst = n >> 6, ch = (n & 63) >> 3;
+      *reinterpret_cast<uint2*>(ha + kst * (HA_B / 2) + ml * 64 + swz(ml, ch) * 8 + (n & 7)) =
+          *reinterpret_cast<const uint2*>(h);
+    }
+  }
+  auto issue = [&](int st) {   // proj_out weight stage st (K [64 st, +64)) into slot st & 1
+    const unsigned base = lds0 + (unsigned)(SL0 + (st & 1) * W2_B);
+#pragma unroll
+    for (int i = 0; i < W2_INS; ++i) {
+      const int qq = wv + 8 * i;
+      dma16s(rw3, vo3, __builtin_amdgcn_readfirstlane((8 * qq * C + 64 * st) * 2),
+             __builtin_amdgcn_readfirstlane(base + qq * 1024));
+    }
+  };
+  issue(0);
+  issue(1);
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < KS1; ++st) {
+    if (st + 1 < KS1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(W2_INS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // stage st and every h image landed
+    const uint4* Ws = smem + (SL0 + (st & 1) * W2_B) / 16;
+    const uint4* Hs = smem + (HA0 + st * HA_B) / 16;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      Frag8<bf16_t> hf[FM];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int ml = 32 * wm + 16 * i + lr;
+        hf[i].v = Hs[ml * 8 + swz(ml, 4 * ks + g)];
+      }
+#pragma unroll
+      for (int j = 0; j < FN2; ++j) {
+        const int r = 160 * wn + 16 * j + lr;
+        Frag8<bf16_t> wf;
+        wf.v = Ws[r * 8 + swz(r, 4 * ks + g)];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) mma_k32(acc[i][j], wf, hf[i]);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+#pragma unroll
+      for (int j = 0; j < FN2 - 1; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (st + 2 < KS1) {
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every wave is done with slot st & 1
+      issue(st + 2);
+    }
+  }
+  // out = bf16(acc + b_po) staged over the h images, then the PRE row writer (residual x_in,
+  // GroupNorm partials, 16-B row stores)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  bf16_t* stg = reinterpret_cast<bf16_t*>(smem);
+#pragma unroll
+  for (int j = 0; j < FN2; ++j) {
+    const int n = 160 * wn + 16 * j + 4 * g;
+    const float4 b4 = p3.bias ? *reinterpret_cast<const float4*>(p3.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int ml = 32 * wm + 16 * i + lr;
+      bf16_t h[4] = {f2bf(acc[i][j][0] + b4.x), f2bf(acc[i][j][1] + b4.y), f2bf(acc[i][j][2] + b4.z),
+                     f2bf(acc[i][j][3] + b4.w)};
+      *reinterpret_cast<uint2*>(stg + ml * HP + n) = *reinterpret_cast<const uint2*>(h);
+    }
+  }
+  __syncthreads();
+  int tid_late = tid;
+  asm volatile("" : "+v"(tid_late));
+  epilogue_fast<BM, C, NT, true>(p3, m0, 0, stg, HP, reinterpret_cast<float*>(smem) + BM * HP / 2, tid_late);
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, const ConvArgs p2, const ConvArgs p3) {
   using namespace ffk;
   __shared__ uint4 smem[LDS_B / 16];
   const int F = p2.kpad;                  // hidden width (FF2 K)
@@ -119,13 +245,19 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
   float* const sc1 = sb1 + 2 * MAXF;
   float* const sb2 = sc1 + 2 * MAXF;
 
-  // the GEGLU column constants (packed bias, LayerNorm-fold column sums) once per block: a global
-  // load inside the stage loop would make hipcc drain the weight stream (vmcnt(0)) before its use
-  for (int i = tid; i < g1.n; i += NT) {
-    sb1[i] = g1.bias ? g1.bias[i] : 0.f;
-    sc1[i] = g1.ln_rows ? g1.ln_c1[i] : 0.f;
-  }
-  for (int i = tid; i < C; i += NT) sb2[i] = p2.bias ? p2.bias[i] : 0.f;
+  // the GEGLU column constants (packed bias, LayerNorm-fold column sums) in LDS: a global load
+  // inside the stage loop would make hipcc drain the weight stream (vmcnt(0)) before its use.
+  // Staged per tile when the proj_out stages overwrite them after the chunk loop.
+  auto stage_cols = [&]() {
+    for (int i = tid; i < g1.n; i += NT) {
+      sb1[i] = g1.bias ? g1.bias[i] : 0.f;
+      sc1[i] = g1.ln_rows ? g1.ln_c1[i] : 0.f;
+    }
+    for (int i = tid; i < C; i += NT) sb2[i] = p2.bias ? p2.bias[i] : 0.f;
+  };
+  const bool po = p3.w != nullptr;
+  const __amdgpu_buffer_rsrc_t rw3 = __builtin_amdgcn_make_buffer_rsrc((void*)(po ? p3.w : p2.w), 0, po ? p3.w_bytes : 0, kBufFlags);
+  if (!po) stage_cols();
 
   const int vo1 = (drow * g1.kpad + 8 * dchunk) * 2, vo2 = (drow * F + 8 * dchunk) * 2;
   // stage st of chunk c: W1 K stage st (< 5) or the W2 stage (5), into its fixed LDS region
@@ -156,6 +288,7 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
   const int tiles = (M + BM - 1) / BM;
   for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int m0 = tile * BM;
+    if (po) stage_cols();   // (ordered before its first use by the stage loop's barriers)
     // the first chunk's W1 stages fly while x and the LayerNorm rows load
 #pragma unroll
     for (int st = 0; st < KS1; ++st) issue(0, st);
@@ -285,6 +418,10 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
       }
     }
 
+    if (po) {
+      proj_out_tile(p2, p3, rw3, m0, acc2, smem, lds0, tid, wv, lane);
+      continue;
+    }
     // ---- epilogue: bf16(acc + b2) staged over the ring, then the PRE row writer (residual, row
     //      statistics, 16-B row stores)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // every wave left the ring / H
@@ -315,7 +452,8 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
 
 // ---------------------------------------------------------------------------------------
 // host side
-extern "C" int ldm_feedforward(const ldm_conv_params* g, const ldm_conv_params* f, ldm_stream_t stream) {
+extern "C" int ldm_feedforward(const ldm_conv_params* g, const ldm_conv_params* f, const ldm_conv_params* po,
+                               ldm_stream_t stream) {
   using namespace ffk;
   if (!g || !f) return LDM_ERR_ARG;
   const auto a16 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; };
@@ -332,7 +470,17 @@ extern "C" int ldm_feedforward(const ldm_conv_params* g, const ldm_conv_params* 
       g->gn_partial || f->gn_partial || f->ln_rows || g->out_f32 || f->out_f32)
     return LDM_ERR_ARG;
   if (g->ln_rows && !g->ln_c1) return LDM_ERR_ARG;
-  if (!g->a0 || !g->w || !f->w || !f->out) return LDM_ERR_ARG;
+  if (!g->a0 || !g->w || !f->w || (!f->out && !po)) return LDM_ERR_ARG;
+  if (po) {   // proj_out behind the feed-forward: h is not stored
+    if (po->dtype != LDM_BF16 || po->ksize != 1 || po->stride != 1 || po->upsample || po->a1 || po->c1 ||
+        po->c0 != C || po->n != C || po->kpad != C || po->out_layout != LDM_OUT_NHWC || po->act != LDM_ACT_NONE ||
+        po->temb || po->row_stats || po->ln_rows || po->out_f32 || !po->w || !po->out || f->row_stats ||
+        (int64_t)po->batch * po->h_out * po->w_out != M)
+      return LDM_ERR_ARG;
+    if (po->gn_partial && ((po->h_out * po->w_out) % 64 || C % (po->gn_unit > 0 ? po->gn_unit : 1)))
+      return LDM_ERR_ARG;
+    if (!a16(po->w) || !a16(po->out) || !a16(po->residual) || !a16(po->bias)) return LDM_ERR_ALIGN;
+  }
   if (!a16(g->a0) || !a16(g->w) || !a16(f->w) || !a16(f->out) || !a16(f->residual) || !a16(f->bias) ||
       !a16(f->row_stats) || (g->ln_rows && !a16(g->ln_rows)))
     return LDM_ERR_ALIGN;
@@ -368,7 +516,25 @@ extern "C" int ldm_feedforward(const ldm_conv_params* g, const ldm_conv_params* 
   a2.ksplit = 1;
   const int tiles = (int)((M + BM - 1) / BM);
   const int grid = tiles < 256 ? tiles : 256;
-  hipLaunchKernelGGL(feedforward_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, a1, a2);
+  ConvArgs a3{};
+  if (po) {
+    a3.w = (const char*)po->w;
+    a3.w_bytes = C * C * 2;
+    a3.n = C;
+    a3.kpad = C;
+    a3.bias = po->bias;
+    a3.residual = (const char*)po->residual;
+    a3.out = (char*)po->out;
+    a3.out_layout = LDM_OUT_NHWC;
+    a3.act = LDM_ACT_NONE;
+    a3.M = (int)M;
+    a3.hw_out = po->h_out * po->w_out;
+    a3.ksplit = 1;
+    a3.gn_part = po->gn_partial;
+    a3.gn_unit = po->gn_unit > 0 ? po->gn_unit : 1;
+    a3.gn_slots = po->gn_slots > 0 ? po->gn_slots : 1;
+  }
+  hipLaunchKernelGGL(feedforward_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, a1, a2, a3);
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }

@@ -537,6 +537,15 @@ class UNet(nn.Module):
         and ff.net.2 GEMMs separately (A/B — the results are the same bit for bit)."""
         self._ff_fused = bool(enabled)
 
+    @property
+    def ff_proj_out_fused(self):
+        return getattr(self, "_ff_po_fused", True)
+
+    def set_ff_proj_out_fused(self, enabled=True):
+        """With the fused feed-forward: also run Transformer2DModel.proj_out in the same launch
+        (default on; results identical to the separate proj_out call)."""
+        self._ff_po_fused = bool(enabled)
+
     def _transformer(self, P, t, x, B, H, W, ehs):
         p = P[id(t)]
         C = x.shape[-1]
@@ -571,6 +580,9 @@ class UNet(nn.Module):
             h = K.linear(q2["out"], a, residual=h, out=h)
         if rs3 is not None and self.ff_fused and K.feedforward_ok(p["ff1_ln"], p["ff2"], h):
             # ff.net.2(GEGLU(ff.net.0(norm3(h)))) + h in one launch, the 4C intermediate on chip
+            if self.ff_proj_out_fused:     # + proj_out in the same launch (h never stored)
+                return K.feedforward(p["ff1_ln"], p["ff2"], h, ln=(rs3, p["ln_eps"][1]), residual=h,
+                                     proj_out=(p["proj_out"], x, B, H, W, True))
             h = K.feedforward(p["ff1_ln"], p["ff2"], h, ln=(rs3, p["ln_eps"][1]), residual=h, out=h)
             return K.conv2d(p["proj_out"], h, B, H, W, residual=x, gn_stats=True)
         if rs3 is not None:

@@ -70,7 +70,7 @@ EXPORTS = {
     "ldm_conv2d_set_wide": (None, [_i]),
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
-    "ldm_feedforward": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
+    "ldm_feedforward": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp, _i64, _vp]),
     "ldm_attention_fp8_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
@@ -660,11 +660,16 @@ def feedforward_ok(pc1: PackedConv, pc2: PackedConv, x):
             and -(-rows // 128) >= FF_MIN_TILES)
 
 
-def feedforward(pc1: PackedConv, pc2: PackedConv, x, *, ln=None, residual=None, out=None, row_stats=None):
+def feedforward(pc1: PackedConv, pc2: PackedConv, x, *, ln=None, residual=None, out=None, row_stats=None,
+                proj_out=None):
     """FeedForward(GEGLU) in one launch (ldm_feedforward): out = Linear2(h * gelu(g)) (+ residual)
     with [h | g] = Linear1(x) (LayerNorm-folded when ln = (rows, eps) and pc1 is a packed_ln_fold
     weight).  Equal bit for bit to linear(pc2, linear(pc1, x, out_layout=OUT_GEGLU, ln=ln),
-    residual=residual, out=out, row_stats=row_stats); x [..., 320]."""
+    residual=residual, out=out, row_stats=row_stats); x [..., 320].
+
+    proj_out = (pc_po, x_in, batch, h, w, gn_stats): Transformer2DModel.proj_out applied behind it
+    in the same launch (h never stored): returns conv2d(pc_po, ff_out, batch, h, w, residual=x_in,
+    gn_stats=gn_stats) instead, as NHWC [batch, h, w, 320] with the GroupNorm accumulators attached."""
     lib = load_library()
     _gpu(x, pc1.w, pc2.w, residual, out, row_stats)
     _contig(x, "x")
@@ -675,7 +680,25 @@ def feedforward(pc1: PackedConv, pc2: PackedConv, x, *, ln=None, residual=None, 
         raise ValueError("feedforward: pc1 must be the GEGLU pack [2F][C] and pc2 the [C][F] pack")
     if x.dtype != pc1.dtype:
         raise TypeError("feedforward: x dtype != packed weight dtype")
-    if out is None:
+    po_params, po_out, part = None, None, None
+    if proj_out is not None:
+        pc3, x_in, pb, ph, pw, gn_stats = proj_out
+        _gpu(pc3.w, x_in)
+        if pc3.ksize != 1 or pc3.n != C or pc3.kpad != C or pc3.dtype != x.dtype or pb * ph * pw != rows:
+            raise ValueError("feedforward: proj_out must be a 1x1 [320][320] pack over the same rows")
+        if out is not None or row_stats is not None:
+            raise ValueError("feedforward: with proj_out the feed-forward's output is not stored")
+        if x_in is not None and (x_in.numel() != rows * C or x_in.dtype != x.dtype or not x_in.is_contiguous()):
+            raise ValueError("feedforward: proj_out residual must match the output")
+        po_out = torch.empty(pb, ph, pw, C, dtype=x.dtype, device=x.device)
+        unit, slots = 0, 0
+        if gn_stats and rows % 64 == 0 and (ph * pw) % 64 == 0:
+            unit, slots = gn_unit_for(C), gn_slots_for(ph * pw)
+            part = _gn_accumulators(pb, slots, C // unit, x.device)
+        po_params = ConvParams(None, None, C, 0, pb, ph, pw, ph, pw, 1, 1, 0, _ptr(pc3.w), C, C, _ptr(pc3.bias),
+                               None, 0, _ptr(x_in), _ptr(po_out), OUT_NHWC, ACT_NONE, dtype_code(x.dtype), 0, None,
+                               0, _ptr(part), 0, unit, slots, None, None, None, 0.0, 0.0)
+    elif out is None:
         out = torch.empty(x.shape[:-1] + (C,), dtype=x.dtype, device=x.device)
     elif out.numel() != rows * C or out.dtype != x.dtype or not out.is_contiguous():
         raise ValueError("feedforward: preallocated out has the wrong size / dtype / layout")
@@ -700,10 +723,13 @@ def feedforward(pc1: PackedConv, pc2: PackedConv, x, *, ln=None, residual=None, 
                    _ptr(residual), _ptr(out), OUT_NHWC, ACT_NONE, dt, 0, None, 0, None, 0, 0, 0, _ptr(row_stats),
                    None, None, 0.0, 0.0)
     ev = _prof_start()
-    _check(lib.ldm_feedforward(ctypes.byref(g), ctypes.byref(f), _stream(x)), "ldm_feedforward")
-    setattr(out, GN_PART_ATTR, None)
+    _check(lib.ldm_feedforward(ctypes.byref(g), ctypes.byref(f), None if po_params is None else ctypes.byref(po_params),
+                               _stream(x)), "ldm_feedforward")
+    if po_out is not None:
+        out = po_out
+    setattr(out, GN_PART_ATTR, part)
     if ev is not None:
-        flops = 2.0 * rows * (2 * F * C + C * F)
+        flops = 2.0 * rows * (2 * F * C + C * F + (C * C if po_out is not None else 0))
         nbytes = (x.numel() + out.numel() + (0 if residual is None else residual.numel())) * x.element_size() + \
             (pc1.w.numel() + pc2.w.numel()) * pc1.w.element_size()
         _prof_stop(ev, "igemm", flops, nbytes, f"ff M={rows} C={C} F={F}")
