@@ -421,6 +421,40 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
       glds16(vs, vb + off);
     }
   };
+  // full tiles from per-lane pointers advanced by one tile of rows (attn_d40_kernel's form)
+  constexpr int NSL = (RCH + NW - 1) / NW;
+  const char* kq[NSL];
+  const char* vq[NSL];
+  int64_t kstep[NSL], vstep[NSL];
+#pragma unroll
+  for (int s2 = 0; s2 < NSL; ++s2) {
+    const int i = wave + NW * s2;
+    const int L = i * 64 + lane;
+    const int row = L / RCH, c = L - row * RCH;
+    const bool dat = i < RCH && c < CPR && c * EPC < p.d;
+    const bool kone = MC && c == p.d / EPC;
+    const bool vone = c == ones_chunk;
+    kq[s2] = dat ? reinterpret_cast<const char*>(kp + (int64_t)(KVT + row) * p.ks + c * EPC)
+                 : reinterpret_cast<const char*>(kone ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
+    vq[s2] = dat ? reinterpret_cast<const char*>(vp + (int64_t)(KVT + row) * p.vs + c * EPC)
+                 : reinterpret_cast<const char*>(vone ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
+    kstep[s2] = dat ? (int64_t)KVT * p.ks * ES : 0;
+    vstep[s2] = dat ? (int64_t)KVT * p.vs * ES : 0;
+  }
+  auto issue_full = [&](int buf) {   // the next full tile (tiles 1, 2, ... in order)
+    const unsigned kb = lds0 + (unsigned)(buf * 2 * TILE * ES);
+    const unsigned vb = kb + TILE * ES;
+#pragma unroll
+    for (int s2 = 0; s2 < NSL; ++s2) {
+      const int i = wave + NW * s2;
+      if (i >= RCH) break;
+      const unsigned off = __builtin_amdgcn_readfirstlane(i * 64 * 16);
+      glds16(kq[s2], kb + off);
+      glds16(vq[s2], vb + off);
+      kq[s2] += kstep[s2];
+      vq[s2] += vstep[s2];
+    }
+  };
   const float c2 = p.scale_log2;
 
   // Q fragments: x32 chunk c: lane holds Q[q][32c + 8g .. +8] (zero past head_dim; MC: * c2,
@@ -598,7 +632,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int t = 0; t < nfull; ++t) {
-    if (t + 1 < ntiles) issue_tile((t + 1) * KVT, (t + 1) & 1);
+    if (t + 1 < nfull) issue_full((t + 1) & 1);
+    else if (t + 1 < ntiles) issue_tile((t + 1) * KVT, (t + 1) & 1);
     compute(t & 1, t * KVT, false, t == 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
