@@ -315,7 +315,14 @@ def main_sample(args):
     sched = make_scheduler(dev)
     vae_image = GeneralVAEImage().to(dev, dtype).eval()
     vae_seg = GeneralVAESeg(in_channels=16, int_channels=256, out_channels=128, block_out_channels=(32, 64, 128, 256),
-                            num_upscalers=2, scaling_factor=0.2).to(dev, dtype).eval()
+                            num_upscalers=2, scaling_factor=0.2)
+    # random-init logits are too flat for any segment to pass mask_th / count_th: sharpen the last
+    # conv as tests/test_gpu_fullsize.py does, so the timed head runs its keep / relabel work
+    # (trainers_ldm_cond.py:1274-1336) on surviving segments
+    with torch.no_grad():
+        vae_seg.decoder[10].weight.mul_(20.0)
+        vae_seg.decoder[10].bias.sub_(1.0).mul_(20.0)
+    vae_seg = vae_seg.to(dev, dtype).eval()
     B, L = args.frames, parse_latent(args.latent)[0]
     steps = args.steps if args.steps != 20 else 3        # default: 3 timed clips
     warm = min(args.warmup, 1)

@@ -23,8 +23,13 @@ import torch.distributed as dist  # noqa: E402
 
 
 def _moments(st):
-    st.consolidate_state_dict()                           # collective under ZeRO, no-op otherwise
-    sd = st.state_dict()
+    if st.zero:                                           # collective per call; rank `to` keeps the moments
+        for dst in range(st.world):
+            st.consolidate_state_dict(to=dst)
+            if st.rank == dst:
+                sd = st.state_dict()
+    else:
+        sd = st.state_dict()
     return torch.cat([torch.cat([v["exp_avg"].reshape(-1), v["exp_avg_sq"].reshape(-1)]).cpu()
                       for _, v in sorted(sd["state"].items())])
 

@@ -117,3 +117,18 @@ def test_optimizer_state_is_torch_adamw_format():
         assert float(mine["state"][i]["step"]) == float(theirs["state"][i]["step"])
     ref2 = _reference_adamw(_unet(2), 1e-4, 0.01, 0.0, lr_func)
     ref2.load_state_dict(mine)                             # native -> torch AdamW loads it
+
+
+def test_train_step_keeps_inference_ln_fold():
+    """LDMTrainStep turns the LayerNorm fold off for its own forward/backward; for_inference()
+    gives validation sampling the module's original (folded) setting back, and the next
+    train_step turns it off again (the fold was silently lost for inference)."""
+    from ldmseg.schedulers import DDIMNoiseScheduler
+    from ldmseg.trainers.ldm import LDMTrainStep
+    u = _unet(0)
+    assert u.ln_fold
+    ts = LDMTrainStep(u, DDIMNoiseScheduler())
+    assert not u.ln_fold
+    with ts.for_inference() as m:
+        assert m is u and u.ln_fold
+    assert not u.ln_fold

@@ -23,9 +23,11 @@ def test_flat_params_views_and_buckets():
     ps = [torch.nn.Parameter(torch.randn(s)) for s in [(10, 3), (7,), (100,), (5, 5)]]
     vals = [p.detach().clone() for p in ps]
     fp = FlatParams(ps)
-    assert fp.numel == 30 + 7 + 100 + 25
+    # offsets at 16-byte boundaries (ldm_repack / AdamW vector loads): 7 floats are followed by a gap of 1
+    assert fp.offsets == [0, 32, 40, 140] and fp.numel == 30 + 2 + 7 + 1 + 100 + 25
     for p, v in zip(ps, vals):
         assert torch.equal(p.detach(), v)
+        assert p.data.data_ptr() % 16 == 0
         assert p.data.data_ptr() >= fp.data.data_ptr()
         assert p.grad.shape == p.shape
     fp.data.add_(1.0)

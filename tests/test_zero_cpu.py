@@ -45,8 +45,19 @@ def _worker(rank, world, port, q, tmp):
             refused = False
         except RuntimeError:
             refused = True
-        ts.consolidate_state_dict()           # collective: every rank
-        mine = ts.state_dict()
+        ts.consolidate_state_dict()           # collective: every rank; only rank 0 keeps the moments
+        kept_on_host = rank != 0 or all(t.device.type == "cpu" for t in ts._consolidated[1:])
+        if rank != 0:                         # not the consolidating rank: nothing kept, state_dict refuses
+            try:
+                ts.state_dict()
+                refused = False
+            except RuntimeError:
+                pass
+        for dst in range(world):              # each rank's own consolidation (collective per call)
+            ts.consolidate_state_dict(to=dst)
+            if rank == dst:
+                mine = ts.state_dict()
+        released = ts._consolidated is None   # consumed by state_dict()
         theirs = ref.state_dict()
         # checkpoint.save on every rank: consolidated collectively, written by rank 0 only
         from ldmseg.utils import checkpoint
@@ -60,15 +71,17 @@ def _worker(rank, world, port, q, tmp):
         ts2 = LDMTrainStep(_unet(2), DDIMNoiseScheduler(), lr=1e-4, weight_decay=0.01, weight_decay_norm=0.0,
                            lr_factor_func=lr_func, zero_redundancy=True)
         ts2.load_state_dict(saved)
-        ts2.consolidate_state_dict()
-        back = ts2.state_dict()
+        for dst in range(world):
+            ts2.consolidate_state_dict(to=dst)
+            if rank == dst:
+                back = ts2.state_dict()
         same_resumed = all(torch.equal(back["state"][i][k], theirs["state"][i][k])
                            for i in theirs["state"] for k in ("exp_avg", "exp_avg_sq"))
         same = mine["state"].keys() == theirs["state"].keys() and all(
             torch.equal(mine["state"][i][k], theirs["state"][i][k])
             for i in theirs["state"] for k in ("exp_avg", "exp_avg_sq"))
         q.put((rank, ts.shard, ts.exp_avg.numel(), ts.flat.numel, [list(s[:2]) for s in ts.seg_hp],
-               [s[:2] for s in ts.shard_segments()], same and refused and same_saved and same_resumed, ts.step_count,
+               [s[:2] for s in ts.shard_segments()], same and refused and same_saved and same_resumed and kept_on_host and released, ts.step_count,
                ts.flat.data.numpy().copy()))   # by value
     finally:
         dist.destroy_process_group()

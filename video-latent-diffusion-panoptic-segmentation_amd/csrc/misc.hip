@@ -444,9 +444,11 @@ __global__ __launch_bounds__(256) void repack_kernel(const ldm_repack_desc* __re
     lim = (e.ci - r0) * T;
     return c < e.co ? ((int64_t)co * e.ci + r0) * T : -1;
   };
-  if ((e.ci * T) % 4 == 0) {
-    // 16-byte loads: every run starts 16-byte aligned (c0 * T, r0 * T and ci * T are multiples of 4)
-    // and is a whole number of float4; independent loads, all in flight
+  if ((e.ci * T) % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    // 16-byte loads: every run starts 16-byte aligned (a 16-byte aligned source; c0 * T, r0 * T and
+    // ci * T are multiples of 4) and is a whole number of float4; independent loads, all in flight.
+    // A source that is not 16-byte aligned (FlatParams aligns its offsets, other callers may not)
+    // takes the scalar loop below
     const int run4 = run / 4;
     for (int idx = tid; idx < nsrc * run4; idx += 256) {
       const int sr = idx / run4, x = 4 * (idx - sr * run4);

@@ -24,7 +24,14 @@ class FlatParams:
 
     ``pad_to`` (>= the parameters' total) sizes the data storage: ``self.storage`` holds
     ``pad_to`` elements (the tail zero) and ``self.data`` is its first ``numel``, so a ZeRO-1
-    all-gather of equal shards can write straight into it."""
+    all-gather of equal shards can write straight into it.
+
+    Every offset is a multiple of ``ALIGN`` floats (16 bytes): the packed-weight refresh
+    (ldm_repack) and the fused AdamW read their sources with 16-byte vector loads.  A parameter
+    whose numel is not a multiple of 4 is followed by a zero gap (never written by the backward,
+    so the gradient there stays 0 and the gap adds nothing to the clip norm)."""
+
+    ALIGN = 4
 
     def __init__(self, params, device=None, pad_to=None):
         params = list(params)
@@ -32,11 +39,7 @@ class FlatParams:
             raise ValueError("no trainable parameters")
         device = device or params[0].device
         self.params = params
-        self.offsets = []
-        n = 0
-        for p in params:
-            self.offsets.append(n)
-            n += p.numel()
+        self.offsets, n = self.layout(params)
         self.numel = n
         self.storage = torch.zeros(max(n, pad_to or 0), dtype=torch.float32, device=device)
         self.data = self.storage[:n]
@@ -47,6 +50,16 @@ class FlatParams:
             p.data = self.data[o:o + k].view(p.shape)
             p.grad = self.grad[o:o + k].view(p.shape)
         self.index = {id(p): i for i, p in enumerate(params)}
+
+    @classmethod
+    def layout(cls, params):
+        """(offsets, total) of ``params`` laid out back to back at ALIGN-float boundaries."""
+        offsets, n = [], 0
+        for p in params:
+            n = -(-n // cls.ALIGN) * cls.ALIGN
+            offsets.append(n)
+            n += p.numel()
+        return offsets, n
 
     def view_of(self, p, flat):
         i = self.index[id(p)]

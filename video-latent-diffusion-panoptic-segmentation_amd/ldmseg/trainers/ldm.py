@@ -29,6 +29,7 @@ rank's parameters — the same arithmetic, element for element, as the unsharded
 Not native (raises): ohem_ratio < 1, rgb/cond noise levels > 0, inpainting masks,
 prob_train_on_pred > 0 — all off in base.yaml / train_diffusion.sh.
 """
+import contextlib
 import struct
 
 import torch
@@ -82,10 +83,13 @@ def unet_backward_order(unet):
 class LDMTrainStep:
     def __init__(self, unet, scheduler, lr=1e-4, weight_decay=0.0, weight_decay_norm=0.0, betas=(0.9, 0.999),
                  eps=1e-8, clip_grad=3.0, lr_factor_func=None, self_condition=False, min_noise_level=0,
-                 compute_dtype=torch.bfloat16, bucket_mb=100, group=None, seed=None, zero_redundancy=False):
+                 compute_dtype=torch.bfloat16, bucket_mb=100, group=None, seed=None, zero_redundancy=False,
+                 inplace_gather=False):
         self.unet, self.sched = unet, scheduler
         # the training forward differentiates separate LayerNorms; with the fold off every pack is a
-        # plain layout of its parameters, refreshed in place after each update (models/repack.py)
+        # plain layout of its parameters, refreshed in place after each update (models/repack.py).
+        # The module's inference setting is restored inside ``for_inference()`` (validation sampling)
+        self._inference_fold = unet.ln_fold
         unet.set_ln_fold(False)
         self.refresher = PackRefresher(unet)
         self.self_condition = self_condition
@@ -102,7 +106,10 @@ class LDMTrainStep:
         # ZeRO-1 shards are S elements (a multiple of 64) so the all-gather moves equal pieces;
         # the flat storage is padded to S x world once, so the gather writes straight into it
         self.zero = bool(zero_redundancy) and self.world > 1
-        n = sum(p.numel() for p in order)
+        # RCCL in-place all-gather straight into the padded flat storage (no 3.26 GB temporary);
+        # opt-in until a multi-GPU RCCL run has checked it against the out-of-place form
+        self.inplace_gather = bool(inplace_gather)
+        n = FlatParams.layout(order)[1]
         self.shard_len = -(-n // (64 * self.world)) * 64 if self.zero else n
         self.flat = FlatParams(order, dev, pad_to=self.shard_len * self.world if self.zero else None)
         self.bucketer = GradBucketer(self.flat, bucket_mb * 2 ** 20, group)
@@ -178,12 +185,13 @@ class LDMTrainStep:
         return buf[:self.flat.numel]
 
     def _gather_parameters(self):
-        """ZeroRedundancyOptimizer.step's parameter sync: every rank's updated shard to all.  On
-        RCCL an in-place all-gather into the padded flat storage (this rank's shard is already in
-        place: no temporary); gloo (no CUDA all-gather) sums zero-padded copies."""
+        """ZeroRedundancyOptimizer.step's parameter sync: every rank's updated shard to all.  By
+        default through _full (an out-of-place all-gather on RCCL, a sum of zero-padded copies on
+        gloo, which has no CUDA all-gather).  With ``inplace_gather`` (RCCL only) the all-gather
+        writes straight into the padded flat storage, whose own shard is already in place."""
         S, r = self.shard_len, self.rank
         st = self.flat.storage
-        if dist.get_backend(self.group) == "nccl":
+        if self.inplace_gather and dist.get_backend(self.group) == "nccl":
             dist.all_gather_into_tensor(st, st[r * S:(r + 1) * S], group=self.group)
         else:
             lo, hi = self.shard
@@ -218,24 +226,35 @@ class LDMTrainStep:
         d.pop("params")
         return d
 
-    def consolidate_state_dict(self):
-        """ZeroRedundancyOptimizer.consolidate_state_dict: COLLECTIVE under ZeRO (every rank of
-        the group must call it); gathers the sharded AdamW moments so that state_dict() can then
-        be called on any rank alone (e.g. rank 0 inside checkpoint.save).  No-op without ZeRO."""
-        if self.zero:
-            self._consolidated = (self.step_count, self._full(self.exp_avg), self._full(self.exp_avg_sq))
+    def consolidate_state_dict(self, to=0):
+        """ZeroRedundancyOptimizer.consolidate_state_dict(to): COLLECTIVE under ZeRO (every rank
+        of the group must call it); gathers the sharded AdamW moments.  Only rank ``to`` (a rank of
+        the group) keeps them, in host memory, so that state_dict() can then be called there alone
+        (rank 0 inside checkpoint.save); the other ranks keep nothing, and the GPU temporaries of
+        the gather are released before this returns.  No-op without ZeRO."""
+        if not self.zero:
+            return
+        keep = self.rank == to
+        moments = []
+        for m in (self.exp_avg, self.exp_avg_sq):
+            full = self._full(m)
+            moments.append(full.cpu() if keep else None)
+            del full
+        self._consolidated = (self.step_count, *moments) if keep else None
 
     def state_dict(self):
         """torch.optim.AdamW.state_dict() of the same optimizer (fp32 moments, ``step``).  Local
-        (never a collective).  Under ZeRO it needs consolidate_state_dict() on every rank first,
-        as torch's ZeroRedundancyOptimizer does, and raises otherwise — a rank-0-only save can
-        then never block inside a collective the other ranks do not join."""
+        (never a collective).  Under ZeRO it needs consolidate_state_dict(to=this rank) on every
+        rank first, as torch's ZeroRedundancyOptimizer does, and raises otherwise — a rank-0-only
+        save can then never block inside a collective the other ranks do not join.  The
+        consolidated host copy is consumed: it is released once the state dict is built."""
         if self.zero:
             c = self._consolidated
             if c is None or c[0] != self.step_count:
-                raise RuntimeError("ZeRO optimizer state is sharded: call consolidate_state_dict() on every "
-                                   "rank (checkpoint.save does) before state_dict()")
+                raise RuntimeError("ZeRO optimizer state is sharded: call consolidate_state_dict(to=rank) on every "
+                                   "rank (checkpoint.save does) before state_dict() on that rank")
             exp_avg, exp_avg_sq = c[1], c[2]
+            self._consolidated = None
         else:
             exp_avg, exp_avg_sq = self.exp_avg, self.exp_avg_sq
         state, pgs, idx = {}, [], 0
@@ -304,6 +323,22 @@ class LDMTrainStep:
                             *[b for b in self.unet.buffers()])
         self.unet.invalidate_packed()
 
+    @contextlib.contextmanager
+    def for_inference(self):
+        """Inference with the module's own LayerNorm-fold setting (the fused QKV / feed-forward
+        forms) between training iterations, e.g. validation sampling:
+
+            with trainer.for_inference():
+                latents = sample_latents(unet, ...)
+
+        The packs are rebuilt for the folded plan on entry and for the training plan on exit
+        (one prepare() each way)."""
+        self.unet.set_ln_fold(self._inference_fold)
+        try:
+            yield self.unet
+        finally:
+            self.unet.set_ln_fold(False)
+
     def _sink(self, p):
         return self.flat.view_of(p, self.flat.grad), False
 
@@ -311,6 +346,8 @@ class LDMTrainStep:
     def train_step(self, latents, rgb_latents, loss_mask=None, timesteps=None, noise=None):
         """One iteration; returns the (local) mean loss as a 0-d fp64 device tensor."""
         u, sch = self.unet, self.sched
+        if u.ln_fold:                                       # re-enabled by the caller since construction
+            u.set_ln_fold(False)
         B = latents.shape[0]
         dev = latents.device
         if noise is None:
