@@ -169,6 +169,32 @@ int ldm_feedforward(const ldm_conv_params* geglu, const ldm_conv_params* ff2, co
                     ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * ldm_transformer_in — the input half of a Transformer2DModel as ONE launch: the GroupNorm
+ * (Transformer2DModel.norm, from the producer's unit accumulators), proj_in, and norm1 folded
+ * into the fused to_q/k/v GEMM.
+ * Replaces: diffusers Transformer2DModel  h = proj_in(norm(x));  qkv = to_qkv(norm1(h))
+ * (unet.py:361-425) — i.e. ldm_group_norm + ldm_conv2d(proj_in, row_stats) + ldm_conv2d(qkv, ln_rows).
+ *   gn:      the GroupNorm: acc = the fp64 [batch][slots][C / unit][2] unit accumulators the
+ *            producer's epilogue summed (ldm_conv2d gn_partial), groups, eps, gamma / beta [C];
+ *            no activation (the transformer's GroupNorm has none);
+ *   proj_in: 1x1, a0 = x [M][320] bf16 (the raw, un-normalised input), w [320][320], bias, out = h
+ *            [M][320] (to_out's residual); batch / h_out / w_out: the images (h_out * w_out % 128 == 0);
+ *   qkv:     1x1, w = the packed_ln_fold [960][320] weight, bias, ln_c1, ln_inv_k, ln_eps, out =
+ *            qkv [M][960]; a0 and ln_rows are ignored (h and its row statistics stay on chip).
+ * Scope: bf16, width 320 (the 64x64 UNet level).  h and qkv equal the three separate calls bit
+ * for bit (same GroupNorm arithmetic, MFMA sequence per element, row-statistics summation order
+ * and bf16 rounding points). */
+typedef struct {
+  const double* acc;       /* [batch][slots][C / unit][2] fp64 (sum, sumsq) */
+  int unit, slots, groups;
+  float eps;
+  const float* gamma;      /* [C] */
+  const float* beta;       /* [C] */
+} ldm_gn_fold;
+int ldm_transformer_in(const ldm_gn_fold* gn, const ldm_conv_params* proj_in, const ldm_conv_params* qkv,
+                       ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).
  * Replaces: diffusers Attention(AttnProcessor) self-attention attn1 (and cross-attention
  * attn2 when not removed, unet.py:83-105): softmax(Q K^T * scale) V per (batch, head).

@@ -122,6 +122,31 @@ def ff_case(rows, fused=True, Fh=1280, proj_out=False):
     return run, 2.0 * rows * 3 * Fh * C, None
 
 
+def tin_case(B, fused=True):
+    """Transformer2DModel input half at the 64x64 level: GroupNorm -> proj_in -> LN-folded QKV, as
+    ldm_transformer_in or the three launches it replaces."""
+    C, HW = 320, 64
+    B = max(1, B * BATCH // 8)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x_raw = torch.randn(B, HW, HW, C, device=DEV, generator=g).to(BF)
+    pcc = K.PackedConv(torch.randn(C, C, device=DEV, generator=g) * 0.05, None, BF)
+    pc_in = K.PackedConv(torch.randn(C, C, device=DEV, generator=g) * 0.05, torch.randn(C, device=DEV), BF)
+    pc_q = K.packed_ln_fold(torch.randn(3 * C, C, device=DEV, generator=g) * 0.05, None,
+                            torch.ones(C, device=DEV), torch.zeros(C, device=DEV), BF)
+    x = K.conv2d(pcc, x_raw, B, HW, HW, gn_stats=True)
+    gam, bet = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
+    N = HW * HW
+
+    def run():
+        if fused:
+            return K.transformer_in(pc_in, pc_q, x, B, N, 32, gam, bet, 1e-6, 1e-5)
+        h = K.group_norm(x, B, N, 32, gam, bet, 1e-6)
+        rs = torch.zeros(2 * B * N, dtype=torch.float64, device=DEV)
+        h = K.linear(pc_in, h, row_stats=rs)
+        return K.linear(pc_q, h, ln=(rs, 1e-5))
+    return run, 2.0 * B * N * C * 4 * C, None
+
+
 def gn_case(B, HW, C, stats):
     x = torch.randn(B, HW, C, device=DEV).to(BF)
     if stats:
@@ -188,6 +213,8 @@ CASES = {
     "conv3_l1_in_320": lambda: conv_case(8, 32, 32, 320, 640, temb=True, stats=True),
     "conv3_l1_res_640": lambda: conv_case(8, 32, 32, 640, 640, residual=True, stats=True),
     "conv3_l2_in_640": lambda: conv_case(8, 16, 16, 640, 1280, temb=True, stats=True),
+    "tin_l0": lambda: tin_case(8),
+    "tin_l0_unfused": lambda: tin_case(8, fused=False),
     "ff_l0": lambda: ff_case(8 * 4096),
     "ff_l0_unfused": lambda: ff_case(8 * 4096, fused=False),
     "ff_po_l0": lambda: ff_case(8 * 4096, proj_out=True),

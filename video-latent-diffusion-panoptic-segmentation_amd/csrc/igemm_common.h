@@ -651,7 +651,7 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
           float st[8];
           unpack8(packed, st);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) { rsum[q0 + q] += st[k]; rsq[q0 + q] += st[k] * st[k]; }
+          for (int k = 0; k < 8; ++k) { rsum[q0 + q] += st[k]; rsq[q0 + q] = fmaf(st[k], st[k], rsq[q0 + q]); }
         }
       }
     }

@@ -158,7 +158,7 @@ __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x0, const 
       const int c = cc[k] + e;
       const float2 ms = gst[c / cpg];
       sc[k][e] = ms.y * gamma[c];
-      sh[k][e] = beta[c] - ms.x * sc[k][e];
+      sh[k][e] = fmaf(-ms.x, sc[k][e], beta[c]);   // explicit FMAs: ldm_transformer_in repeats them
     }
   }
   for (int r0 = r_beg + ty; r0 < r_end; r0 += UNR * RB) {
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void gn_apply(const T* __restrict__ x0, const 
         T* o = reinterpret_cast<T*>(&res);
 #pragma unroll
         for (int j = 0; j < EPC; ++j) {
-          float y = to_f(e[j]) * sc[k][j] + sh[k][j];
+          float y = fmaf(to_f(e[j]), sc[k][j], sh[k][j]);
           if (act == LDM_ACT_SILU) y = silu_f(y);
           o[j] = from_f<T>(y);
         }

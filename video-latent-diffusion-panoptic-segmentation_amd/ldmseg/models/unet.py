@@ -538,6 +538,16 @@ class UNet(nn.Module):
         self._ff_fused = bool(enabled)
 
     @property
+    def tin_fused(self):
+        return getattr(self, "_tin_fused", True)
+
+    def set_tin_fused(self, enabled=True):
+        """bf16 inference with the LayerNorm fold: run the 64x64 level's GroupNorm -> proj_in ->
+        norm1-folded QKV as one ldm_transformer_in launch (default on; K.transformer_in_ok decides
+        per call); off runs the three launches (A/B — the results are the same bit for bit)."""
+        self._tin_fused = bool(enabled)
+
+    @property
     def ff_proj_out_fused(self):
         return getattr(self, "_ff_po_fused", True)
 
@@ -550,15 +560,21 @@ class UNet(nn.Module):
         p = P[id(t)]
         C = x.shape[-1]
         N = H * W
-        h = K.group_norm(x, B, N, t.groups, *p["norm"], 1e-6)
         cross = p["attn2"] is not None and ehs is not None
         if self.ln_fold and "qkv_ln" in p:
-            rs1 = K.zeroed_f64(2 * B * N, x.device)
             rs3 = None if cross else K.zeroed_f64(2 * B * N, x.device)
-            h = K.linear(p["proj_in"], h, row_stats=rs1)                 # [B, N, C] + row (sum, sumsq)
-            qkv = K.linear(p["qkv_ln"], h, ln=(rs1, p["ln_eps"][0]))      # = to_qkv(norm1(h))
+            if self.tin_fused and K.transformer_in_ok(p["proj_in"], p["qkv_ln"], x, B, N, t.groups):
+                # norm -> proj_in -> norm1-folded QKV in one launch (h and its row statistics on chip)
+                h, qkv = K.transformer_in(p["proj_in"], p["qkv_ln"], x, B, N, t.groups, *p["norm"], 1e-6,
+                                          p["ln_eps"][0])
+            else:
+                h = K.group_norm(x, B, N, t.groups, *p["norm"], 1e-6)
+                rs1 = K.zeroed_f64(2 * B * N, x.device)
+                h = K.linear(p["proj_in"], h, row_stats=rs1)             # [B, N, C] + row (sum, sumsq)
+                qkv = K.linear(p["qkv_ln"], h, ln=(rs1, p["ln_eps"][0]))  # = to_qkv(norm1(h))
         else:
             rs3 = None
+            h = K.group_norm(x, B, N, t.groups, *p["norm"], 1e-6)
             h = K.linear(p["proj_in"], h)                                # [B, N, C]
             n = K.layer_norm(h, *p["ln1"], 1e-5)
             qkv = K.linear(p["qkv"], n)                                  # [B, N, 3C]

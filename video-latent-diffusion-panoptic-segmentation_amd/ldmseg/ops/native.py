@@ -38,6 +38,11 @@ class ConvParams(ctypes.Structure):
                 ("row_stats", _vp), ("ln_rows", _vp), ("ln_c1", _vp), ("ln_inv_k", _f), ("ln_eps", _f)]
 
 
+class GnFold(ctypes.Structure):
+    _fields_ = [("acc", _vp), ("unit", _i), ("slots", _i), ("groups", _i), ("eps", _f), ("gamma", _vp),
+                ("beta", _vp)]
+
+
 class AttnParams(ctypes.Structure):
     _fields_ = [("q", _vp), ("k", _vp), ("v", _vp), ("o", _vp), ("q_stride", _i), ("k_stride", _i),
                 ("v_stride", _i), ("o_stride", _i), ("batch", _i), ("heads", _i), ("head_dim", _i),
@@ -71,6 +76,7 @@ EXPORTS = {
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_feedforward": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
+    "ldm_transformer_in": (_i, [ctypes.POINTER(GnFold), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp, _i64, _vp]),
     "ldm_attention_fp8_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
@@ -734,6 +740,58 @@ def feedforward(pc1: PackedConv, pc2: PackedConv, x, *, ln=None, residual=None, 
             (pc1.w.numel() + pc2.w.numel()) * pc1.w.element_size()
         _prof_stop(ev, "igemm", flops, nbytes, f"ff M={rows} C={C} F={F}")
     return out
+
+
+TIN_WIDTH = 320            # ldm_transformer_in's model width (the 64x64 UNet level)
+
+
+def transformer_in_ok(pc_in: PackedConv, pc_qkv: PackedConv, x, batch, hw, groups):
+    """Whether ldm_transformer_in takes this Transformer2DModel input: bf16, width 320, a
+    LayerNorm-folded QKV pack, whole 128-row tiles per image, producer GroupNorm statistics on x
+    in a layout the kernel stages, and one 128-row tile per CU (fewer run the three-launch form)."""
+    C = x.shape[-1]
+    if not (x.dtype == torch.bfloat16 and pc_in.dtype == torch.bfloat16 and pc_qkv.dtype == torch.bfloat16
+            and C == TIN_WIDTH and pc_in.ksize == 1 and pc_qkv.ksize == 1 and pc_in.n == C and pc_in.kpad == C
+            and pc_qkv.n == 3 * C and pc_qkv.kpad == C and getattr(pc_qkv, "ln_c1", None) is not None
+            and hw % 128 == 0 and batch * hw // 128 >= FF_MIN_TILES and 0 < groups <= 64 and C % groups == 0):
+        return False
+    s0, _, unit, slots = _gn_sources(x, None, batch, C, 0, groups)
+    return s0 is not None and slots * (C // unit) <= 256
+
+
+def transformer_in(pc_in: PackedConv, pc_qkv: PackedConv, x, batch, hw, groups, gamma, beta, gn_eps, ln_eps):
+    """Transformer2DModel's input half in one launch (ldm_transformer_in): returns (h, qkv) with
+    h = linear(pc_in, group_norm(x, ...)) and qkv = linear(pc_qkv, h, ln=(row_stats(h), ln_eps)) —
+    equal bit for bit to the three separate calls; x [batch, hw, 320] with producer statistics."""
+    lib = load_library()
+    _gpu(x, pc_in.w, pc_qkv.w, gamma, beta)
+    _contig(x, "x")
+    C = x.shape[-1]
+    if not transformer_in_ok(pc_in, pc_qkv, x, batch, hw, groups):
+        raise ValueError("transformer_in: call outside ldm_transformer_in's scope (see transformer_in_ok)")
+    if gamma.numel() != C or beta.numel() != C or gamma.dtype != torch.float32 or beta.dtype != torch.float32:
+        raise ValueError("gamma/beta must be fp32 [C]")
+    s0, _, unit, slots = _gn_sources(x, None, batch, C, 0, groups)
+    h = torch.empty(batch, hw, C, dtype=x.dtype, device=x.device)
+    qkv = torch.empty(batch, hw, 3 * C, dtype=x.dtype, device=x.device)
+    gn = GnFold(_ptr(s0), unit, slots, groups, float(gn_eps), _ptr(gamma), _ptr(beta))
+    dt = dtype_code(x.dtype)
+    pi = ConvParams(_ptr(x), None, C, 0, batch, hw, 1, hw, 1, 1, 1, 0, _ptr(pc_in.w), C, C, _ptr(pc_in.bias),
+                    None, 0, None, _ptr(h), OUT_NHWC, ACT_NONE, dt, 0, None, 0, None, 0, 0, 0, None, None, None,
+                    0.0, 0.0)
+    pq = ConvParams(None, None, C, 0, batch, hw, 1, hw, 1, 1, 1, 0, _ptr(pc_qkv.w), 3 * C, C, _ptr(pc_qkv.bias),
+                    None, 0, None, _ptr(qkv), OUT_NHWC, ACT_NONE, dt, 0, None, 0, None, 0, 0, 0, None, None,
+                    _ptr(pc_qkv.ln_c1), 1.0 / C, float(ln_eps))
+    ev = _prof_start()
+    _check(lib.ldm_transformer_in(ctypes.byref(gn), ctypes.byref(pi), ctypes.byref(pq), _stream(x)),
+           "ldm_transformer_in")
+    if ev is not None:
+        rows = batch * hw
+        flops = 2.0 * rows * C * 4 * C
+        nbytes = (x.numel() + h.numel() + qkv.numel()) * x.element_size() + \
+            (pc_in.w.numel() + pc_qkv.w.numel()) * pc_in.w.element_size()
+        _prof_stop(ev, "igemm", flops, nbytes, f"tin M={rows} C={C}")
+    return h, qkv
 
 
 # ======================================================================================
