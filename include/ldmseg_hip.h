@@ -193,6 +193,8 @@ typedef struct {
 } ldm_gn_fold;
 int ldm_transformer_in(const ldm_gn_fold* gn, const ldm_conv_params* proj_in, const ldm_conv_params* qkv,
                        ldm_stream_t stream);
+/* Tuning / A-B hook: kernel variant of ldm_transformer_in (1 = default; see csrc/transformer_in.hip). */
+void ldm_transformer_in_set_mode(int mode);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).

@@ -122,7 +122,7 @@ def ff_case(rows, fused=True, Fh=1280, proj_out=False):
     return run, 2.0 * rows * 3 * Fh * C, None
 
 
-def tin_case(B, fused=True):
+def tin_case(B, fused=True, mode=1):
     """Transformer2DModel input half at the 64x64 level: GroupNorm -> proj_in -> LN-folded QKV, as
     ldm_transformer_in or the three launches it replaces."""
     C, HW = 320, 64
@@ -139,6 +139,7 @@ def tin_case(B, fused=True):
 
     def run():
         if fused:
+            K.set_transformer_in_mode(mode)
             return K.transformer_in(pc_in, pc_q, x, B, N, 32, gam, bet, 1e-6, 1e-5)
         h = K.group_norm(x, B, N, 32, gam, bet, 1e-6)
         rs = torch.zeros(2 * B * N, dtype=torch.float64, device=DEV)
@@ -215,6 +216,9 @@ CASES = {
     "conv3_l2_in_640": lambda: conv_case(8, 16, 16, 640, 1280, temb=True, stats=True),
     "tin_l0": lambda: tin_case(8),
     "tin_l0_unfused": lambda: tin_case(8, fused=False),
+    "tin_l0_m0": lambda: tin_case(8, mode=0),
+    "tin_l0_noload": lambda: tin_case(8, mode=9),
+    "tin_l0_nomfma": lambda: tin_case(8, mode=17),
     "ff_l0": lambda: ff_case(8 * 4096),
     "ff_l0_unfused": lambda: ff_case(8 * 4096, fused=False),
     "ff_po_l0": lambda: ff_case(8 * 4096, proj_out=True),

@@ -65,6 +65,11 @@ __device__ __forceinline__ void tin_wait(int n) {
     case 3: asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 9: asm volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+    case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
     case 15: asm volatile("s_waitcnt vmcnt(15)" ::: "memory"); break;
     case 22: asm volatile("s_waitcnt vmcnt(22)" ::: "memory"); break;
     case 25: asm volatile("s_waitcnt vmcnt(25)" ::: "memory"); break;
@@ -74,10 +79,10 @@ __device__ __forceinline__ void tin_wait(int n) {
 // DMA instructions this wave may leave in flight when it waits for stage u of a 10-stage run:
 // the younger stages (min(5, stages left)) x 3, plus the 10 epilogue stores issued after the
 // previous run's last stage, which are younger than the six stages following it
-__host__ __device__ constexpr int tin_younger(int u, bool last) {
+__host__ __device__ constexpr int tin_younger(int u, bool last, int ins = tik::INS) {
   const int left = last ? tik::S_Q - 1 - u : tik::NSLOT - 2;
   const int ahead = left < tik::NSLOT - 2 ? left : tik::NSLOT - 2;
-  return tik::INS * ahead + (u <= tik::NSLOT - 2 ? tik::EPI_ST : 0);
+  return ins * ahead + (u <= tik::NSLOT - 2 ? tik::EPI_ST : 0);
 }
 static_assert(tin_younger(0, false) == 25 && tin_younger(6, false) == 15 && tin_younger(5, true) == 22 &&
               tin_younger(6, true) == 9 && tin_younger(7, true) == 6 && tin_younger(8, true) == 3 &&
@@ -98,6 +103,14 @@ __device__ __forceinline__ uint32_t pk2(float a, float b) {
   return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
 }
 
+// MODE (tuning / A-B; the default is 1): bit 0 issues a stage's DMA between its two k32 halves
+// (beside the first half's MFMAs) instead of before them (50.7 -> 48.6 us, tools/opbench.py tin_l0);
+// bit 1 drops the dummy DMA instructions (waves 4-7 issue two per stage, counted per wave: 62.7 us,
+// the per-wave counts spill 64 VGPRs); bit 2 gives waves 4-7 static priority 1 (no gain); ablations:
+// bit 3 no weight stream (43.4 us), bit 4 no MFMA (fragments kept live: slower, the reads serialise).
+// What bounds it: the 8 (M) x 1 (N) form reads one 1-KB W fragment per 16x16x32 MFMA, i.e. the LDS
+// array's 256 B/clk exactly when the MFMA pipes are full, so neither runs near its peak.
+template <int MODE>
 __global__ __launch_bounds__(512, 1) void transformer_in_kernel(const ConvArgs pi, const ConvArgs pq,
                                                                 const double* __restrict__ gacc, int gunit,
                                                                 int gslots, int groups, float geps,
@@ -129,6 +142,7 @@ __global__ __launch_bounds__(512, 1) void transformer_in_kernel(const ConvArgs p
   const int vo = (drow * C + 8 * dchunk) * 2;   // lane part of a weight row's source offset (kpad = C)
   // stage s of the tile (0..39): proj_in (s < 10) or QKV chunk (s - 10) / 10; K block kb, N half nh
   auto issue = [&](int s) {
+    if (MODE & 8) return;                          // ablation: no weight stream
     const bool is_in = s < S_IN;
     const int t = is_in ? s : s - S_IN;
     const int u = is_in ? t : t % S_Q;
@@ -139,6 +153,7 @@ __global__ __launch_bounds__(512, 1) void transformer_in_kernel(const ConvArgs p
     for (int i = 0; i < INS; ++i) {
       const int ii = wv + 8 * i;                 // DMA instruction of the stage: rows 8 ii .. 8 ii + 7
       const bool real = ii < SN / 8;
+      if ((MODE & 2) && !real) break;
       const int soff = __builtin_amdgcn_readfirstlane(real ? ((row0 + 8 * ii) * C + 64 * kb) * 2 : kOOB);
       const unsigned dst = __builtin_amdgcn_readfirstlane(real ? base + ii * 1024 : lds0 + DUMMY_OFF);
       if (is_in) dma16s(rwi, vo, soff, dst);
@@ -153,11 +168,15 @@ __global__ __launch_bounds__(512, 1) void transformer_in_kernel(const ConvArgs p
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[h][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   };
-  // one stage: acc[nh] += W_stage (160 x 64) . A[:, 64 kb .. +64)
-  auto mma_stage = [&](int slot, const uint4* af, int nh) {
+  // one stage: acc[nh] += W_stage (160 x 64) . A[:, 64 kb .. +64); `mid` runs between the halves
+  auto mma_stage = [&](int slot, const uint4* af, int nh, auto mid) {
     const uint4* Ws = smem + slot * (STAGE_B / 16);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      if (ks == 1) {
+        mid();
+        __builtin_amdgcn_sched_barrier(0);
+      }
       Frag8<bf16_t> wf[FN], xa;
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
@@ -167,6 +186,10 @@ __global__ __launch_bounds__(512, 1) void transformer_in_kernel(const ConvArgs p
       xa.v = af[ks];
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
+        if (MODE & 16) {                               // ablation: fragments read, no MFMA
+          asm volatile("" ::"v"(wf[j].v.x), "v"(wf[j].v.w), "v"(xa.v.x));
+          continue;
+        }
         if (nh == 0) mma_k32(acc[0][j], wf[j], xa);
         else mma_k32(acc[1][j], wf[j], xa);
       }
@@ -182,6 +205,7 @@ __global__ __launch_bounds__(512, 1) void transformer_in_kernel(const ConvArgs p
     }
   };
 
+  if ((MODE & 4) && wv >= 4) __builtin_amdgcn_s_setprio(1);
   const int tiles = M / BM;
   for (int tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const int m0 = tile * BM;
@@ -245,12 +269,15 @@ __global__ __launch_bounds__(512, 1) void transformer_in_kernel(const ConvArgs p
 
     // ---- proj_in: 10 stages
     zero_acc();
+    const int ins = (MODE & 2) && wv >= 4 ? INS - 1 : INS;
 #pragma unroll
     for (int s = 0; s < S_IN; ++s) {
-      tin_wait(INS * (NSLOT - 2));
+      tin_wait(ins * (NSLOT - 2));
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      issue(s + NSLOT - 1);
-      mma_stage(s % NSLOT, &xf[2 * (s >> 1)], s & 1);
+      if (!(MODE & 1)) issue(s + NSLOT - 1);
+      mma_stage(s % NSLOT, &xf[2 * (s >> 1)], s & 1, [&]() {
+        if (MODE & 1) issue(s + NSLOT - 1);
+      });
     }
     // ---- h = bf16(acc + b_in): to HBM (16-byte stores) and into the QKV A fragments; the
     //      LayerNorm row statistics in the row writer's order
@@ -306,10 +333,13 @@ __global__ __launch_bounds__(512, 1) void transformer_in_kernel(const ConvArgs p
 #pragma unroll
       for (int u = 0; u < S_Q; ++u) {
         const int s = S_IN + S_Q * q + u;
-        tin_wait(last ? tin_younger(u, true) : tin_younger(u, false));
+        if (ins == INS) tin_wait(last ? tin_younger(u, true) : tin_younger(u, false));
+        else tin_wait(last ? tin_younger(u, true, INS - 1) : tin_younger(u, false, INS - 1));
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        if (s + NSLOT - 1 < NST) issue(s + NSLOT - 1);
-        mma_stage(s % NSLOT, &hf[2 * (u >> 1)], u & 1);
+        if (!(MODE & 1) && s + NSLOT - 1 < NST) issue(s + NSLOT - 1);
+        mma_stage(s % NSLOT, &hf[2 * (u >> 1)], u & 1, [&]() {
+          if ((MODE & 1) && s + NSLOT - 1 < NST) issue(s + NSLOT - 1);
+        });
       }
       // rstd (acc - mean c1) + bias -> bf16 -> 16-byte row stores
 #pragma unroll
@@ -337,6 +367,11 @@ __global__ __launch_bounds__(512, 1) void transformer_in_kernel(const ConvArgs p
 
 // ---------------------------------------------------------------------------------------
 // host side
+namespace {
+int g_tin_mode = 1;   // tuning / A-B hook (ldm_transformer_in_set_mode)
+}
+extern "C" void ldm_transformer_in_set_mode(int mode) { g_tin_mode = mode; }
+
 extern "C" int ldm_transformer_in(const ldm_gn_fold* gn, const ldm_conv_params* pin, const ldm_conv_params* qkv,
                                   ldm_stream_t stream) {
   using namespace tik;
@@ -381,8 +416,17 @@ extern "C" int ldm_transformer_in(const ldm_gn_fold* gn, const ldm_conv_params* 
   aq.out = (char*)qkv->out;
   const int tiles = (int)(M / BM);
   const int grid = tiles < 256 ? tiles : 256;
-  hipLaunchKernelGGL(transformer_in_kernel, dim3(grid), dim3(NT), 0, (hipStream_t)stream, ai, aq, gn->acc, gn->unit,
-                     gn->slots, gn->groups, gn->eps, gn->gamma, gn->beta);
+#define TIN_LAUNCH(m)                                                                                     \
+  hipLaunchKernelGGL(transformer_in_kernel<m>, dim3(grid), dim3(NT), 0, (hipStream_t)stream, ai, aq, gn->acc, \
+                     gn->unit, gn->slots, gn->groups, gn->eps, gn->gamma, gn->beta)
+  switch (g_tin_mode) {
+    case 0: TIN_LAUNCH(0); break;
+    case 2: TIN_LAUNCH(2); break;
+    case 9: TIN_LAUNCH(9); break;
+    case 17: TIN_LAUNCH(17); break;
+    default: TIN_LAUNCH(1); break;
+  }
+#undef TIN_LAUNCH
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }

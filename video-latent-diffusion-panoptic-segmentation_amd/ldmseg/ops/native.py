@@ -77,6 +77,7 @@ EXPORTS = {
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_feedforward": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
     "ldm_transformer_in": (_i, [ctypes.POINTER(GnFold), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
+    "ldm_transformer_in_set_mode": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp, _i64, _vp]),
     "ldm_attention_fp8_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
@@ -757,6 +758,11 @@ def transformer_in_ok(pc_in: PackedConv, pc_qkv: PackedConv, x, batch, hw, group
         return False
     s0, _, unit, slots = _gn_sources(x, None, batch, C, 0, groups)
     return s0 is not None and slots * (C // unit) <= 256
+
+
+def set_transformer_in_mode(mode):
+    """Tuning / A-B hook: ldm_transformer_in kernel variant (1 = default)."""
+    load_library().ldm_transformer_in_set_mode(int(mode))
 
 
 def transformer_in(pc_in: PackedConv, pc_qkv: PackedConv, x, batch, hw, groups, gamma, beta, gn_eps, ln_eps):
