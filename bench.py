@@ -77,6 +77,12 @@ def roofline(unet, stepper, ts, nsteps, dtype, fp8=False):
     finally:
         K.set_profiler(None)
     fam = prof.summary()
+    if os.environ.get("LDM_OPLOG"):
+        # the profiled steps' launches in order (tools/traffic_table.py aligns them with the
+        # per-dispatch PMC counters of the same run to attribute HBM traffic per op)
+        with open(os.environ["LDM_OPLOG"], "w") as f:
+            json.dump({"steps": nsteps, "ops": [{"family": r[0], "flops": r[1], "bytes": r[2], "detail": r[5]}
+                                                for r in prof.records]}, f)
     if os.environ.get("LDM_BENCH_DETAIL"):
         det = prof.summary(by_detail=True)
         print(f"{'kernel':10s} {'shape':44s} {'n':>3s} {'ms':>8s} {'TF/s':>7s} {'GB/s':>7s}", file=sys.stderr)

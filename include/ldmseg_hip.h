@@ -127,8 +127,11 @@ void ldm_conv2d_force_stages(int stages);
 /* Tuning hook: M panels per tile-raster group of ldm_conv2d (default 8; 1 = row-major tiles). */
 void ldm_conv2d_set_raster_group(int group_m);
 /* Tuning hook: the halo-tiled 3x3 kernel (bf16, stride 1, 64-channel-aligned sources, output
- * width 64 or 32): 0 = planner's choice, 1 = never, 2 = whenever legal. */
+ * width 64 or 32: 4-row tiles; 16x16 images: whole-image tiles with K split over channel blocks
+ * into an fp32 slab): 0 = planner's choice, 1 = never, 2 = whenever legal. */
 void ldm_conv2d_set_halo(int mode);
+/* Tuning hook: force the split-K factor of the 16x16 whole-image halo tiles (0 = planner). */
+void ldm_conv2d_set_halo_split(int ksplit);
 /* Tuning hook: the A-register-stationary bf16 1x1 GEMM (K = 320, N a multiple of 160, NHWC or
  * GEGLU, no time embedding / GroupNorm partials): 0 = planner's choice (the 64x64 UNet level),
  * 1 = never, 2 = whenever legal. */
@@ -227,6 +230,9 @@ void ldm_attention_set_fp8_scaled(int enabled);
 /* Tuning hook (benchmarks / tests only): 1 routes bf16 through the 16x16x16-MFMA kernel
  * instead of the 16x16x32 one; 0 restores the default. */
 void ldm_attention_force_legacy(int legacy);
+/* Tuning / A-B hook: 1 (default) runs head_dim 80 on the 32x32x16 kernel of head_dim 40, 0 on the
+ * 16x16x32 one. */
+void ldm_attention_set_d80(int enabled);
 /* Tuning / A-B hook: 1 (default) runs the bf16 backward for head_dim <= 64 on the 32x32x16 MFMA
  * kernels, 0 on the 16x16x16 ones. */
 void ldm_attention_set_bwd32(int enabled);

@@ -242,6 +242,30 @@ def test_attention_block_waves(B, N, C, waves):
     assert rel_err(o, ref) < tol(torch.bfloat16)
 
 
+@pytest.mark.parametrize("B,N", [(8, 1024), (1, 300), (2, 64)])
+def test_attention_d80_forms_agree(B, N):
+    """head_dim 80 on the 32x32x16 kernel (the default: the d = 40 kernel's form with a 96-wide
+    Q.K^T and three 32-row P.V blocks) and on the 16x16x32 kernel: both within the bf16 bar of the
+    fp32 reference, and close to each other; the log-sum-exp the training backward reads agrees."""
+    torch.manual_seed(6)
+    C = 640
+    q, k, v = torch.randn(B, N, C), torch.randn(B, N, C), torch.randn(B, N, C)
+    ref = _attn_ref(q, k, v, 8)
+    qkv = torch.cat([q, k, v], -1).to(DEV, torch.bfloat16)
+    outs = []
+    try:
+        for on in (True, False):
+            K.set_attention_d80(on)
+            o, lse = K.attention_fwd_lse(qkv, qkv[..., C:], qkv[..., 2 * C:], B, 8, 80, N, N, 3 * C, 3 * C, 3 * C)
+            outs.append((o.float(), lse.float()))
+    finally:
+        K.set_attention_d80(True)
+    for o, _ in outs:
+        assert rel_err(o, ref) < tol(torch.bfloat16)
+    assert (outs[0][0] - outs[1][0]).abs().max().item() < 0.05
+    assert torch.allclose(outs[0][1], outs[1][1], atol=2e-2)
+
+
 def test_attention_softmax_spike():
     """Force the online-softmax rescale: a huge logit in the LAST kv tile of some rows."""
     torch.manual_seed(4)

@@ -29,9 +29,14 @@ def test_headline_plans_pinned():
     # QKV at K = 320 stays on the two-blocks-per-CU tiles (the wide tile lost there, r03a)
     pl = _p(batch=8 * 4096, h=1, w=1, c0=320, n=960, ksize=1, ln=True, geglu_bias=False)
     assert (pl["kind"], pl["bm"], pl["bn"]) == ("tile", 128, 160), pl
-    # deep K over few tiles: split to 512 blocks
-    pl = _p(batch=8, h=16, w=16, c0=1280, n=1280, temb=True, gn_stats=True)
-    assert (pl["bm"], pl["bn"], pl["ksplit"], pl["blocks"]) == (128, 160, 4, 512), pl
+    # the 16x16 level: whole-image halo tiles (256 rows) split over channel blocks to 256+ blocks
+    for c0, c1, ks in ((1280, 0, 4), (1280, 1280, 4), (1280, 640, 5)):
+        pl = _p(batch=8, h=16, w=16, c0=c0, c1=c1, n=1280, temb=True, gn_stats=True)
+        assert (pl["kind"], pl["bm"], pl["bn"], pl["ksplit"]) == ("halo", 256, 160, ks), pl
+        assert pl["blocks"] >= 256 and (c0 + c1) // 64 // ks >= 4, pl
+    # 640 -> 1280 would need 2-channel-block splits: the split 128x160 tiles stay faster
+    pl = _p(batch=8, h=16, w=16, c0=640, n=1280, temb=True, gn_stats=True)
+    assert (pl["kind"], pl["bm"], pl["bn"], pl["ksplit"]) == ("tile", 128, 160, 4), pl
     pl = _p(batch=8, h=8, w=8, c0=1280, n=1280, temb=True, gn_stats=True)
     assert (pl["bm"], pl["bn"], pl["ksplit"], pl["blocks"]) == (64, 160, 8, 512), pl
     pl = _p(batch=8, h=8, w=8, c0=1280, c1=1280, n=1280, residual=True, gn_stats=True)

@@ -49,10 +49,11 @@ def mm_case(M, K, N):
     return (lambda: torch.mm(a, b)), 2.0 * M * K * N, None
 
 
-def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True):
+def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True, d80=True):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
     def run():
+        K.set_attention_d80(d80)
         K.force_attention_legacy(legacy)
         K.set_attention_waves(waves)
         K.set_attention_maxcol(maxcol)
@@ -250,6 +251,7 @@ CASES = {
     "attn_1024_d80_legacy": lambda: attn_case(8, 1024, 640, legacy=True),
     "attn_256_d160_legacy": lambda: attn_case(8, 256, 1280, legacy=True),
     "attn_1024_d80": lambda: attn_case(8, 1024, 640),
+    "attn_1024_d80_x16": lambda: attn_case(8, 1024, 640, d80=False),
     "attn_4096_d40_w8": lambda: attn_case(8, 4096, 320, waves=8),
     "attn_1024_d80_w8": lambda: attn_case(8, 1024, 640, waves=8),
     "attn_4096_d40_w4": lambda: attn_case(8, 4096, 320, waves=4),

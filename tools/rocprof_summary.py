@@ -28,7 +28,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # (family, regex on the kernel name, is_primary) — primary kernels count calls
 FAMILIES = [
-    ("igemm", r"(igemm_kernel|igemm_big_kernel|conv3_halo_kernel|gemm_ars2?_kernel|gemm_wide_kernel)<|feedforward_kernel", True),
+    ("igemm", r"(igemm_kernel|igemm_big_kernel|conv3_halo_kernel|gemm_ars2?_kernel|gemm_wide_kernel)<|feedforward_kernel|"
+              r"transformer_in_kernel", True),
     ("igemm", r"splitk_epilogue_kernel<", False),
     ("attention", r"attn(32|_d40|_f8)?_kernel<", True),
     ("group_norm", r"gn_apply", True),

@@ -678,11 +678,18 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 // The row max is a tree over the lane's 32 scores plus one permlane32 swap.  Scale and running
 // max ride in the head-dim padding (Q prescaled, Q[:, 40] = -m, K[:, 40] = 1), the softmax
 // denominator in V's ones column (d = 40), as in attn32_kernel's MC / ONES forms.
-template <int NW, int OCC, int KT = 64>
+// Templated on the head dim D (a multiple of 8): D = 40 (the 64x64 level) and D = 80 (the 32x32
+// level).  Q.K^T runs over DQ = D + 1 (the max column) rounded up to 16 (48 / 96: 3 / 6 MFMAs per
+// 32-key block), P.V over ND32 = ceil((D + 1) / 32) 32-row head-dim blocks (2 / 3, the ones column
+// d = D carrying the denominator).
+template <int NW, int OCC, int KT = 64, int D = 40>
 __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p) {
   typedef bf16_t T;
   typedef __attribute__((ext_vector_type(16))) float f32x16_t;
-  constexpr int EPC = 8, CPR = 8, RCH = CPR + 1, ROW = RCH * EPC, TILE = KT * ROW, ES = 2;
+  static_assert(D % 8 == 0, "head dim");
+  constexpr int DQ = (D + 16) / 16 * 16, QC = DQ / 16, ND32 = (D + 32) / 32;
+  constexpr int EPC = 8, CPR = (DQ > 32 * ND32 ? DQ : 32 * ND32) / 8, RCH = CPR + 1, ROW = RCH * EPC,
+                TILE = KT * ROW, ES = 2;
   __shared__ uint4 smem[2 * 2 * TILE * ES / 16];
   T* const lds = reinterpret_cast<T*>(smem);
   typedef __attribute__((address_space(3))) uint4 lds_u4_t;
@@ -705,7 +712,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
   const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
   const T* vp = reinterpret_cast<const T*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * p.d;
-  constexpr int ONES_CHUNK = 5;                     // d = 40: V ones column, K max column
+  constexpr int ONES_CHUNK = D / 8;                 // d = D: V ones column, K max column
 
   auto issue_tile = [&](int kv0, int buf) {
     const unsigned kb = lds0 + (unsigned)(buf * 2 * TILE * ES);
@@ -765,21 +772,21 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   const float c2 = p.scale_log2;
 
   // Q^T (B operand) chunk c: lane holds Q[q = qbase + r32][d = 16c + 8hh .. +8] * c2; the max
-  // column d = 40 is element 0 of chunk 2 in the hh = 1 lanes (initially -m = 0)
-  uint4 qf[3];
+  // column d = D is element 0 of chunk D / 16 in the hh = (D % 16) / 8 lanes (initially -m = 0)
+  uint4 qf[QC];
   {
     const int qi = qbase + r32;
     const T* qrow = qp + (int64_t)qi * p.qs;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) {
+    for (int c = 0; c < QC; ++c) {
       const int dd = 16 * c + 8 * hh;
       if (qi < p.nq && dd < p.d) qf[c] = scale_bf16x8(*reinterpret_cast<const uint4*>(qrow + dd), c2);
       else qf[c] = make_uint4(0u, 0u, 0u, 0u);
     }
   }
-  f32x16_t oacc[2];
+  f32x16_t oacc[ND32];
 #pragma unroll
-  for (int db = 0; db < 2; ++db)
+  for (int db = 0; db < ND32; ++db)
 #pragma unroll
     for (int r = 0; r < 16; ++r) oacc[db][r] = 0.f;
   float mq = 0.f;
@@ -798,7 +805,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
       for (int r = 0; r < 16; ++r) sacc[blk][r] = 0.f;
       const T* krow = Ks + (32 * blk + r32) * ROW + 8 * hh;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
+      for (int c = 0; c < QC; ++c) {
         const uint4 ka = *reinterpret_cast<const uint4*>(krow + 16 * c);
         sacc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, ka),
                                                             __builtin_bit_cast(bf16x8_t, qf[c]), sacc[blk], 0, 0, 0);
@@ -834,11 +841,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
       const float delta = mn - mq;
       const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);   // (O = 0 on the first tile)
       mq = mn;
-      oacc[0] *= alpha;
-      oacc[1] *= alpha;
+#pragma unroll
+      for (int db = 0; db < ND32; ++db) oacc[db] *= alpha;
       sacc[0] -= delta;
       sacc[1] -= delta;
-      if (hh == 1) qf[2].x = (qf[2].x & 0xffff0000u) | (__float_as_uint(-mn) >> 16);
+      if (hh == (D % 16) / 8) qf[D / 16].x = (qf[D / 16].x & 0xffff0000u) | (__float_as_uint(-mn) >> 16);
     }
     uint4 pb[2][2];                           // bf16 P^T fragment of k-step (block, s)
 #pragma unroll
@@ -853,7 +860,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
       }
     // O^T += V^T P^T: A = V^T rows d (block db) for keys 16s' + {4hh..+3, 8 + 4hh..+3} of block blk
 #pragma unroll
-    for (int db = 0; db < 2; ++db) {
+    for (int db = 0; db < ND32; ++db) {
       const int cb = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
 #pragma unroll
       for (int blk = 0; blk < 2; ++blk)
@@ -886,22 +893,25 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
     for (int hf = 0; hf < KT / 64 && nfull * KT + 64 * hf < p.nkv; ++hf) compute(nfull & 1, nfull * KT, true, nfull == 0, hf);
   }
 
-  // denominator: O^T row d = 40 = block 1 register 4 of the hh = 0 lane of this column
-  const float lt = __shfl(oacc[1][4], r32, 64);
+  // denominator: O^T row d = D = block D / 32, register 4 ((D % 32) / 8) of the hh = 0 lane of this
+  // column (a 32x32 result row 8 (r >> 2) + 4 hh + (r & 3) sits in register r of the hh half)
+  static_assert(D % 8 == 0, "denominator row");
+  const float lt = __shfl(oacc[D / 32][4 * ((D % 32) / 8)], r32, 64);
   const float inv = 1.0f / lt;
   const int qi = qbase + r32;
   if (qi < p.nq) {
     if (p.lse && hh == 0) p.lse[((int64_t)b * p.heads + h) * p.nq + qi] = mq + __log2f(lt);
     T* orow = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * p.d + (int64_t)qi * p.os;
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = 8 * g4 + 4 * hh;
-      *reinterpret_cast<uint2*>(orow + d) =
-          make_uint2(pack_bf16x2(oacc[0][4 * g4] * inv, oacc[0][4 * g4 + 1] * inv),
-                     pack_bf16x2(oacc[0][4 * g4 + 2] * inv, oacc[0][4 * g4 + 3] * inv));
-    }
-    *reinterpret_cast<uint2*>(orow + 32 + 4 * hh) =
-        make_uint2(pack_bf16x2(oacc[1][0] * inv, oacc[1][1] * inv), pack_bf16x2(oacc[1][2] * inv, oacc[1][3] * inv));
+    for (int db = 0; db < ND32; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * db + 8 * g4 + 4 * hh;
+        if (32 * db + 8 * g4 >= D) break;          // (compile-time: D % 8 == 0)
+        *reinterpret_cast<uint2*>(orow + d) =
+            make_uint2(pack_bf16x2(oacc[db][4 * g4] * inv, oacc[db][4 * g4 + 1] * inv),
+                       pack_bf16x2(oacc[db][4 * g4 + 2] * inv, oacc[db][4 * g4 + 3] * inv));
+      }
   }
 }
 
@@ -950,8 +960,21 @@ int launch32_dp_mc(const AttnArgs& a, int batch, hipStream_t s) {
   return launch32_cfg<DP, QS0, false, F8, MC>(a, batch, s);
 }
 
+int g_attn_d80 = 1;      // tuning / A-B hook: 0 routes head_dim 80 to the 16x16x32 kernel
+
 template <int DP, bool F8 = false>
 int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
+  if constexpr (DP == 80) {
+    if (!F8 && g_attn_d80 && a.d == 80) {
+      // the 32x32x16 form at head_dim 80 (the 32x32 level): 8 waves x 32 queries per block
+      const int nb8 = (a.nq + 255) / 256 * a.heads * batch;
+      if (nb8 >= 256) hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80>), dim3(nb8), dim3(512), 0, s, a);
+      else hipLaunchKernelGGL((attn_d40_kernel<4, 2, 64, 80>), dim3((a.nq + 127) / 128 * a.heads * batch),
+                              dim3(256), 0, s, a);
+      LDM_CHECK_LAUNCH();
+      return LDM_OK;
+    }
+  }
   // the max column pays at head_dim 40 (N=4096: 273 -> 252 us); at 80 it costs occupancy
   // (134 vs 122 VGPRs: 39.7 -> 41.0 us), so it is kept to DP = 48
   if constexpr (DP == 48) {
@@ -2024,6 +2047,7 @@ extern "C" void ldm_attention_set_fp8_scaled(int enabled) { g_fp8_scaled = enabl
 extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 || waves == 8) ? waves : 0; }
 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
+extern "C" void ldm_attention_set_d80(int enabled) { g_attn_d80 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_bwd32(int enabled) { g_attn_bwd32 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_maxcol(int mode) {
   g_attn_maxcol = mode >= 1 ? 1 : 0;     // 0: per-score FMA, 16x16x32 kernel

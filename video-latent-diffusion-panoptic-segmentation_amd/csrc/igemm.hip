@@ -810,13 +810,18 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
     const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
     tile = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
   }
+  // split-K over channel blocks (the 16x16 level's whole-image tiles): split `split` of ksplit
+  // runs channel blocks [cb0, cb1) and writes an fp32 partial slab; a tile's splits are adjacent ids
+  const int split = tile % p.ksplit;
+  tile /= p.ksplit;
   int tm, tn;
   grouped_tile(tile, p.M / BM, p.tiles_n, p.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int b = m0 / p.hw_out;
   const int oy0 = (m0 - b * p.hw_out) / W;
-  const int ncb = p.cin / 64;
-  const int nsteps = 9 * ncb;
+  const int ncb_all = p.cin / 64;
+  const int cb0 = ncb_all * split / p.ksplit, cb1 = ncb_all * (split + 1) / p.ksplit;
+  const int nsteps = 9 * (cb1 - cb0);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
@@ -859,7 +864,7 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
   const int rr = tid >> 3, cc = tid & 7;               // rr in [0, 64)
   const int cl = cc ^ ((rr >> 1) & 7);                 // (rr + 64 i) >> 1 & 7 == rr >> 1 & 7
   auto issue_b = [&](int s) {
-    const int cb = s / 9, tap = s - 9 * (s / 9);
+    const int cb = cb0 + s / 9, tap = s - 9 * (s / 9);
     const int kb = (tap * p.cin + cb * 64 + 8 * cl) * 2;
     const unsigned base = lds_b + (unsigned)((s % NBS) * B_U4 * 16);
 #pragma unroll
@@ -887,7 +892,7 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
     hp0[i] = oyl * HW + ox;
   }
   auto compute = [&](int s) {
-    const int cb = s / 9, tap = s - 9 * (s / 9);
+    const int cb = cb0 + s / 9, tap = s - 9 * (s / 9);
     const int ky = tap / 3, kx = tap - 3 * ky;
     const uint4* As = smem + (cb & 1) * HALO_U4;
     const uint4* Bs = smem + 2 * HALO_U4 + (s % NBS) * B_U4;
@@ -912,26 +917,26 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
     }
   };
 
-  // prologue: the whole halo of channel block 0 and B of step 0
+  // prologue: the whole halo of channel block cb0 and B of step 0
 #pragma unroll
   for (int t = 0; t < A_TAPS; ++t)
-    if (has_piece(t)) issue_halo(0, t);
+    if (has_piece(t)) issue_halo(cb0, t);
   issue_b(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
-    const int cb = s / 9, tap = s - 9 * (s / 9);
+    const int cb = cb0 + s / 9, tap = s - 9 * (s / 9);
     if (s > 0) {
       // issued by this wave after B(s) (at step s - 1): the halo piece of step s - 1, if any.
       // (A deeper, 3-slot B ring measured slower: 68 -> 74 us on the 64x64 320-channel conv.)
       const int pt = tap == 0 ? 8 : tap - 1;
       const int pcb = tap == 0 ? cb - 1 : cb;
-      if (pcb + 1 < ncb && has_piece(pt)) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      if (pcb + 1 < cb1 && has_piece(pt)) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       asm volatile("s_barrier" ::: "memory");
     }
     if (s + 1 < nsteps) issue_b(s + 1);
-    if (cb + 1 < ncb && has_piece(tap)) issue_halo(cb + 1, tap);
+    if (cb + 1 < cb1 && has_piece(tap)) issue_halo(cb + 1, tap);
     compute(s);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -961,6 +966,10 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
     }
     __syncthreads();
     const int mh = m0 + h * EPI_ROWS;
+    if (p.ksplit > 1) {
+      write_partial_rows<EPI_ROWS, BN, NT>(p, p.partial + (int64_t)split * p.M * p.n, mh, n0, stage, PITCH);
+      continue;
+    }
     if (fast && fast_temb_ok(p, mh, EPI_ROWS)) epilogue_fast<EPI_ROWS, BN, NT>(p, mh, n0, stage, PITCH, red);
     else epilogue_rows<T, EPI_ROWS, BN, NT>(p, mh, n0, raw, red);
   }
@@ -970,23 +979,30 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
 // the kernel is instantiated for, whole output rows per tile
 int g_halo_mode = 0;   // tuning hook: 0 planner, 1 never, 2 whenever legal
 int g_epi_pre = 1;     // tuning hook: bf16 pre-activated staging epilogue (1) or fp32 staging (0)
+// output rows per halo tile: 4 at widths 64 / 32, the whole image at 16 (the 16x16 level, split
+// over channel blocks)
+constexpr int halo_rows(int w) { return w == 64 ? 4 : (w == 32 ? 4 : (w == 16 ? 16 : 0)); }
 bool halo_legal(const ldm_conv_params* q, int es) {
   if (es != 2 || q->ksize != 3 || q->stride != 1 || q->upsample || q->pad_mode != 0) return false;
   if (q->c0 % 64 || q->c1 % 64 || q->kpad != 9 * (q->c0 + q->c1)) return false;
   if (q->h_in != q->h_out || q->w_in != q->w_out) return false;
   if (q->out_layout != LDM_OUT_NHWC || q->out_f32) return false;
   const int W = q->w_out;
-  const int R = W == 64 ? 4 : (W == 32 ? 4 : 0);
-  return R && q->h_out % R == 0;
+  return halo_rows(W) && q->h_out % halo_rows(W) == 0;
 }
+
+template <typename T>
+void launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);
 
 int launch_halo(ConvArgs a, hipStream_t s) {
   a.tiles_n = (a.n + halo::BN - 1) / halo::BN;
-  const int bm = a.w_out * 4;
-  a.nblk = (a.M / bm) * a.tiles_n;
+  const int bm = a.w_out * halo_rows(a.w_out);
+  a.nblk = (a.M / bm) * a.tiles_n * a.ksplit;
   if (a.w_out == 64) hipLaunchKernelGGL((conv3_halo_kernel<64, 4>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
-  else hipLaunchKernelGGL((conv3_halo_kernel<32, 4>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  else if (a.w_out == 32) hipLaunchKernelGGL((conv3_halo_kernel<32, 4>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  else hipLaunchKernelGGL((conv3_halo_kernel<16, 16>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
   LDM_CHECK_LAUNCH();
+  if (a.ksplit > 1) launch_splitk_epilogue<bf16_t>(a, s);
   return LDM_OK;
 }
 
@@ -1272,14 +1288,30 @@ bool is_mixed(const ldm_conv_params* q, int es) {
 // Planner (opbench at the UNet shapes, B=8; igemm -> halo, us): 64 wide: 320->320 76 -> 69,
 // [640||320]->320 191 -> 168; 32 wide: 640->640 84 -> 76, 320->640 45 -> 44, but [1280||640]->640
 // 191 -> 206 (30 channel blocks on the 128-row halo tile lose to the tap-major 128x160 tiles)
-bool use_halo_plan(const ldm_conv_params* q, int es, bool mixed) {
-  if (g_halo_mode == 1 || mixed || g_force_bm || !halo_legal(q, es)) return false;
-  if (g_halo_mode == 2) return true;
+// Halo plan: 0 = none, else the split-K factor (1 = unsplit).
+int g_halo_split = 0;   // tuning hook (ldm_conv2d_set_halo_split): force the 16x16 level's split
+int halo_plan(const ldm_conv_params* q, int es, bool mixed) {
+  if (g_halo_mode == 1 || mixed || g_force_bm || !halo_legal(q, es)) return 0;
+  const int ncb = (q->c0 + q->c1) / 64;
+  if (q->w_out == 16) {
+    // whole 16x16 images (256 rows) x 160 channels, K split over channel blocks toward >= 256 blocks
+    // with >= 4 channel blocks per split (opbench, B = 8, 16x16 level, us incl. the split-K
+    // reduction, halo vs 128x160 x 4 tiles: 1280 -> 1280 76.0 vs 79.3, [1280 || 1280] -> 1280 123.6
+    // vs 134.5; but 640 -> 1280 at 5 splits of 2 channel blocks 70.9 vs 51.8)
+    const int64_t base = (int64_t)q->batch * (q->n / halo::BN);
+    if (q->n % halo::BN) return 0;
+    if (g_halo_split > 0) return std::min(g_halo_split, ncb);
+    for (int ks = 1; ks <= ncb; ++ks)
+      if (ncb % ks == 0 && ncb / ks >= 4 && base * ks >= 256) return ks;
+    return g_halo_mode == 2 ? 1 : 0;
+  }
+  if (g_halo_mode == 2) return 1;
   // >= 256 blocks (one per CU): at B = 1 the 4-row halo tiles give 32 (3x3 320 at 64x64: 69.7 us vs
   // 32.4 on split 64x160 tiles)
   const int64_t blocks = (int64_t)q->batch * q->h_out / 4 * (q->n / halo::BN);
-  return q->n % halo::BN == 0 && blocks >= 256 && (q->w_out == 64 || (q->w_out == 32 && q->c0 + q->c1 <= 960));
+  return (q->n % halo::BN == 0 && blocks >= 256 && (q->w_out == 64 || (q->w_out == 32 && q->c0 + q->c1 <= 960))) ? 1 : 0;
 }
+bool use_halo_plan(const ldm_conv_params* q, int es, bool mixed) { return halo_plan(q, es, mixed) > 0; }
 
 #include "gemm_ars.h"
 
@@ -1298,6 +1330,7 @@ extern "C" void ldm_conv2d_force_plan(int bm, int bn, int ksplit) {
 int g_group_m = 8;
 extern "C" void ldm_conv2d_set_raster_group(int g) { g_group_m = g >= 1 ? g : 8; }
 extern "C" void ldm_conv2d_set_halo(int mode) { g_halo_mode = (mode == 1 || mode == 2) ? mode : 0; }
+extern "C" void ldm_conv2d_set_halo_split(int ks) { g_halo_split = ks > 0 ? ks : 0; }
 extern "C" void ldm_conv2d_set_ars(int mode) { g_ars_mode = (mode >= 1 && mode <= 3) ? mode : 0; }
 extern "C" void ldm_conv2d_set_splitk_cols(int cols) { g_splitk_cols = (cols == 64 || cols == 128) ? cols : 0; }
 extern "C" void ldm_conv2d_set_epilogue(int mode) { g_epi_pre = mode == 1 ? 0 : 1; }
@@ -1310,7 +1343,9 @@ extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   if (validate(q, &es) != LDM_OK) return 0;
   const int M = q->batch * q->h_out * q->w_out;
   const bool mixed = is_mixed(q, es);
-  if (use_halo_plan(q, es, mixed) || ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0) || use_ars(q, es, mixed, M)) return 0;
+  const int hks = halo_plan(q, es, mixed);
+  if (hks) return hks > 1 ? (size_t)hks * M * q->n * sizeof(float) : 0;
+  if (ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0) || use_ars(q, es, mixed, M)) return 0;
   const Plan pl = make_plan(q, M, es, mixed);
   return pl.ksplit > 1 ? (size_t)pl.ksplit * M * q->n * sizeof(float) : 0;
 }
@@ -1322,14 +1357,15 @@ extern "C" int ldm_conv2d_describe_plan(const ldm_conv_params* q, int* out) {
   if (!out) return LDM_ERR_ARG;
   const int M = q->batch * q->h_out * q->w_out;
   const bool mixed = is_mixed(q, es);
-  const bool halo = use_halo_plan(q, es, mixed);
+  const int hks = halo_plan(q, es, mixed);
+  const bool halo = hks > 0;
   const int wbm = halo ? 0 : ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0);
   const bool ars = !halo && !wbm && use_ars(q, es, mixed, M);
   if (halo || wbm || ars) {
     out[0] = halo ? 1 : (wbm ? 2 : 3);
-    out[1] = halo ? q->w_out * 4 : wbm;
+    out[1] = halo ? q->w_out * halo_rows(q->w_out) : wbm;
     out[2] = halo ? halo::BN : (wbm ? 320 : 0);
-    out[3] = 1;
+    out[3] = halo ? hks : 1;
     out[4] = 0;
     return LDM_OK;
   }
@@ -1350,10 +1386,11 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   const int cin = q->c0 + q->c1;
   const int M = q->batch * q->h_out * q->w_out;
   const bool mixed = is_mixed(q, es);
-  const bool use_halo = use_halo_plan(q, es, mixed);
+  const int hks = halo_plan(q, es, mixed);
+  const bool use_halo = hks > 0;
   const int wbm = use_halo ? 0 : ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0);
   const bool ars = !use_halo && !wbm && use_ars(q, es, mixed, M);
-  const Plan pl = (use_halo || wbm || ars) ? Plan{0, 0, 1} : make_plan(q, M, es, mixed);
+  const Plan pl = use_halo ? Plan{0, 0, hks} : ((wbm || ars) ? Plan{0, 0, 1} : make_plan(q, M, es, mixed));
   if (pl.ksplit > 1) {
     const size_t need = (size_t)pl.ksplit * M * q->n * sizeof(float);
     if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;

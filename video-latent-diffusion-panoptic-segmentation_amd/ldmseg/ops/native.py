@@ -71,6 +71,7 @@ EXPORTS = {
     "ldm_conv2d_force_stages": (None, [_i]),
     "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_conv2d_set_halo": (None, [_i]),
+    "ldm_conv2d_set_halo_split": (None, [_i]),
     "ldm_conv2d_set_ars": (None, [_i]),
     "ldm_conv2d_set_wide": (None, [_i]),
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
@@ -97,6 +98,7 @@ EXPORTS = {
     "ldm_gaussian_posterior": (_i, [_vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _i, _vp]),
     "ldm_attention_fwd_lse": (_i, [ctypes.POINTER(AttnParams), _vp, _vp]),
     "ldm_attention_force_legacy": (None, [_i]),
+    "ldm_attention_set_d80": (None, [_i]),
     "ldm_attention_set_bwd32": (None, [_i]),
     "ldm_conv2d_wgrad_set_ring": (None, [_i]),
     "ldm_attention_set_waves": (None, [_i]),
@@ -542,7 +544,7 @@ def describe_plan(batch, h, w, c0, n, *, c1=0, ksize=3, stride=1, upsample=False
     if kind == 0 or kind == 4:
         blocks = -(-M // bm) * -(-n // bn) * ks
     elif kind == 1:
-        blocks = M // bm * (n // bn)
+        blocks = M // bm * (n // bn) * ks
     else:
         blocks = -(-M // bm) * (n // bn) if bn else None
     return {"kind": PLAN_KINDS[kind], "bm": bm, "bn": bn, "ksplit": ks, "stages": st, "blocks": blocks}
@@ -594,6 +596,11 @@ def set_attention_bwd32(enabled=True):
     load_library().ldm_attention_set_bwd32(int(bool(enabled)))
 
 
+def set_attention_d80(enabled=True):
+    """Tuning / A-B hook: head_dim 80 on the 32x32x16 kernel (default) or the 16x16x32 one."""
+    load_library().ldm_attention_set_d80(int(bool(enabled)))
+
+
 def force_attention_legacy(legacy=True):
     """Tuning hook: route bf16 attention through the 16x16x16-MFMA kernel (A/B only)."""
     load_library().ldm_attention_force_legacy(int(bool(legacy)))
@@ -612,6 +619,11 @@ def set_conv_raster_group(group_m=8):
 def set_conv_halo(mode=0):
     """Tuning hook: halo-tiled 3x3 kernel — 0 planner, 1 never, 2 whenever legal."""
     load_library().ldm_conv2d_set_halo(int(mode))
+
+
+def set_conv_halo_split(ks=0):
+    """Tuning hook: split-K factor of the 16x16 whole-image halo tiles (0 = planner)."""
+    load_library().ldm_conv2d_set_halo_split(int(ks))
 
 
 def set_conv_ars(mode=0):
