@@ -198,6 +198,53 @@ def test_conv_transpose_shuffle(dt):
     assert rel_err(y.permute(0, 3, 1, 2), ref) < tol(dt)
 
 
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("B,cin,cout,H,W", [(2, 320, 320, 16, 16), (8, 1280, 1280, 8, 8), (1, 640, 640, 32, 32),
+                                             (2, 64, 96, 4, 8), (3, 128, 160, 8, 12)])
+def test_upsample_conv_phases(B, cin, cout, H, W, dt):
+    """Upsample2D's conv in phase form (four 2x2 convs over the low-res input, ldm_conv2d upsample
+    mode 3) vs torch conv3x3(nearest_upsample_2x(x)) in fp32, and its GroupNorm partials through a
+    following GroupNorm; the 3x3 gather form of the same conv for comparison."""
+    torch.manual_seed(21)
+    x = torch.randn(B, cin, H, W)
+    w = torch.randn(cout, cin, 3, 3) / (3 * cin ** 0.5)
+    b = torch.randn(cout)
+    ref = F.conv2d(F.interpolate(x, scale_factor=2, mode="nearest"), w, b, padding=1)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV, dt)
+    pcp = K.PackedConv(w.to(DEV), b.to(DEV), dt, upsample_phases=True)
+    y = K.conv2d(pcp, xn, B, H, W, upsample=True, gn_stats=True)
+    assert rel_err(y.permute(0, 3, 1, 2), ref) < tol(dt)
+    y3 = K.conv2d(K.PackedConv(w.to(DEV), b.to(DEV), dt), xn, B, H, W, upsample=True)
+    assert rel_err(y, y3) < tol(dt)
+    if cout % 32 == 0 and (4 * H * W) % 64 == 0:
+        assert K.gn_stats_of(y) is not None
+        gam, bet = torch.randn(cout), torch.randn(cout)
+        out = K.group_norm(y, B, 4 * H * W, 32, gam.to(DEV), bet.to(DEV), 1e-5, K.ACT_SILU)
+        gref = F.silu(F.group_norm(ref, 32, gam, bet, 1e-5))
+        assert rel_err(out.view(B, 2 * H, 2 * W, -1).permute(0, 3, 1, 2), gref) < (3e-4 if dt == torch.float32 else 3e-2)
+
+
+def test_upsample_phases_unet_close_to_gather_form():
+    """The whole UNet with the phase-form Upsample2D convs (default) against the 3x3 gather form:
+    the same function up to the bf16 rounding of the summed taps."""
+    from ldmseg.models import UNet
+    torch.manual_seed(0)
+    with torch.device(DEV):
+        u = UNet()
+    u.remove_cross_attention()
+    u.modify_encoder(in_channels=8, init_mode_seg="copy", init_mode_image="zero")
+    u = u.to(torch.bfloat16).eval()
+    x = torch.randn(8, 8, 64, 64, device=DEV).to(torch.bfloat16)
+    t = torch.full((8,), 500, device=DEV, dtype=torch.long)
+    with torch.no_grad():
+        u.set_upsample_phases(False)
+        y0 = u(x, t).sample.float().clone()
+        u.set_upsample_phases(True)
+        y1 = u(x, t).sample.float()
+    torch.cuda.synchronize()
+    assert rel_err(y1, y0) < 2e-2
+
+
 # ------------------------------------------------------------------------------ attention
 def _attn_ref(q, k, v, heads):
     B, N, C = q.shape

@@ -23,13 +23,13 @@ BATCH = 8          # --batch: the conv / GEMM cases' B (their shapes are written
 
 
 def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, geglu=False, residual=False,
-              temb=False, stats=False, c1=0):
+              temb=False, stats=False, c1=0, phases=False):
     B = max(1, B * BATCH // 8)
     g = torch.Generator(device=DEV).manual_seed(0)
     x0 = torch.randn(B, H, W, Cin - c1, device=DEV, generator=g).to(BF)
     x1 = torch.randn(B, H, W, c1, device=DEV, generator=g).to(BF) if c1 else None
     w = torch.randn(Cout, Cin, k, k, device=DEV, generator=g) * 0.05
-    pc = K.PackedConv(w, torch.randn(Cout, device=DEV), BF, geglu=geglu)
+    pc = K.PackedConv(w, torch.randn(Cout, device=DEV), BF, geglu=geglu, upsample_phases=phases)
     ho, wo = (2 * H, 2 * W) if up else ((H - 1) // stride + 1, (W - 1) // stride + 1)
     res = torch.randn(B, ho, wo, Cout, device=DEV).to(BF) if residual else None
     te = torch.randn(B, Cout, device=DEV) if temb else None
@@ -38,7 +38,7 @@ def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, ge
     def run():
         return K.conv2d(pc, x0, B, H, W, x1=x1, stride=stride, upsample=up, residual=res, temb=te,
                         temb_stride=Cout if temb else 0, out_layout=out_layout, gn_stats=stats)
-    flops = 2.0 * B * ho * wo * Cout * k * k * Cin
+    flops = 2.0 * B * ho * wo * Cout * (4 if phases else k * k) * Cin     # executed (phase form: 4 taps)
     return run, flops, None
 
 
@@ -199,6 +199,11 @@ CASES = {
     "gemm_proj_640": lambda: conv_case(8, 32, 32, 640, 640, k=1, residual=True),
     "conv3_up_l1_1920": lambda: conv_case(8, 32, 32, 1920, 640, c1=640, residual=True, stats=True),
     "conv3_upsample_320": lambda: conv_case(8, 32, 32, 640, 640, up=True, stats=True),
+    "conv3_upsample_640_ph": lambda: conv_case(8, 32, 32, 640, 640, up=True, stats=True, phases=True),
+    "conv3_upsample_1280": lambda: conv_case(8, 16, 16, 1280, 1280, up=True, stats=True),
+    "conv3_upsample_1280_ph": lambda: conv_case(8, 16, 16, 1280, 1280, up=True, stats=True, phases=True),
+    "conv3_upsample_l3": lambda: conv_case(8, 8, 8, 1280, 1280, up=True, stats=True),
+    "conv3_upsample_l3_ph": lambda: conv_case(8, 8, 8, 1280, 1280, up=True, stats=True, phases=True),
     "conv3_l2_up_2560": lambda: conv_case(8, 16, 16, 2560, 1280, c1=1280, residual=True, stats=True),
     "gemm_proj_1280_l2": lambda: conv_case(8, 16, 16, 1280, 1280, k=1, residual=True),
     "gemm_proj_1280_l3": lambda: conv_case(8, 8, 8, 1280, 1280, k=1, residual=True),

@@ -89,7 +89,14 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     const int b = m / p.hw_out;
     const int pix = m - b * p.hw_out;
     const int oy = pix / p.w_out, ox = pix - oy * p.w_out;
-    if (p.upsample) {           // coordinates in the 2x upsampled input
+    if (p.phase) {              // 2x2 taps of phase (dy, dx) at input rows y - 1 + dy .. y + dy
+      const int hwl = p.hw_out >> 2, wl = p.w_out >> 1;
+      const int ph = pix / hwl, q = pix - ph * hwl;
+      const int y = q / wl, x = q - y * wl;
+      iy0[i] = y - 1 + (ph >> 1);
+      ix0[i] = x - 1 + (ph & 1);
+      pix0[i] = (b * p.h_in + iy0[i]) * p.w_in + ix0[i];
+    } else if (p.upsample) {    // coordinates in the 2x upsampled input
       iy0[i] = oy - p.pad;
       ix0[i] = ox - p.pad;
       pix0[i] = b * p.h_in;
@@ -123,9 +130,12 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
     }
     return ok ? (pixel * cs + choff) * ES : kOOB;
   };
+  // phase mode: the tile's rows share one phase (hw_out / 4 is a multiple of BM), whose weights
+  // are the phase-th [n][kpad] block
+  const int wrow0 = p.phase ? ((m0 % p.hw_out) / (p.hw_out >> 2)) * p.n : 0;
   auto b_offset = [&](int i) -> int {
     const int n = n0 + rr + 32 * i;
-    return (n < p.n) ? (n * p.kpad + ks_.kofs) * ES : kOOB;
+    return (n < p.n) ? ((wrow0 + n) * p.kpad + ks_.kofs) * ES : kOOB;
   };
   auto advance = [&]() { ks_.advance(p, BK); };
 
@@ -1085,7 +1095,30 @@ Plan make_plan_base(const ldm_conv_params* q, int M, int es, bool mixed_src);
 
 // row statistics / LayerNorm fold: unsplit tiles of the 2-blocks-per-CU kernel with >= 64 rows;
 // GEGLU on 128x128 (the register epilogue needs a wave N extent of 32k)
+// Phase-form upsample conv (four 2x2 convs over the low-res grid, 4/9 of the 3x3 FLOPs): a tile's
+// rows must lie in one phase, so bm divides hw_out / 4; K split only when the tiles leave the chip
+// half idle (the 8x8 -> 16x16 upsampler at B = 8 gives 256 64x160 tiles of K = 5120).
+Plan phase_plan(const ldm_conv_params* q, int M, int es) {
+  Plan pl;
+  const int hwl = q->h_out * q->w_out / 4;
+  const int nk = q->kpad / (128 / es);
+  pl.bm = hwl % 128 == 0 ? 128 : (hwl % 64 == 0 ? 64 : 32);
+  pl.bn = (es == 2 && pl.bm >= 64 && q->n % 160 == 0) ? 160 : (q->n <= 64 ? 64 : 128);
+  pl.ksplit = 1;
+  if (g_force_bm && hwl % g_force_bm == 0 && (g_force_bm < 256) &&
+      (g_force_bn != 160 || (es == 2 && g_force_bm >= 64))) {
+    pl.bm = g_force_bm;
+    pl.bn = g_force_bn;
+    pl.ksplit = clamp_ksplit(g_force_ks, nk);
+    return pl;
+  }
+  const int tiles = (M / pl.bm) * ((q->n + pl.bn - 1) / pl.bn);
+  if (tiles < 384 && nk >= 32) pl.ksplit = std::max(1, std::min(std::min(8, nk / 16), (512 + tiles / 2) / tiles));
+  return pl;
+}
+
 Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
+  if (q->upsample == 3) return phase_plan(q, M, es);
   Plan pl = make_plan_base(q, M, es, mixed_src);
   // few tiles (config 2's B = 1; the B = 8 plans all give >= 512 blocks): 64x160 tiles split K toward
   // ~512 blocks (profiles/r03g_b1_plans.txt, eager us: 3x3 320 at 64x64 69.7 -> 32.4, 3x3 640 at
@@ -1233,10 +1266,16 @@ int validate(const ldm_conv_params* q, int* es_out) {
   if (q->dtype != LDM_F32 && q->dtype != LDM_BF16) return LDM_ERR_ARG;
   const int es = q->dtype == LDM_F32 ? 4 : 2;
   const int ce = 16 / es;
-  if (q->ksize != 1 && q->ksize != 3 && q->ksize != 5 && q->ksize != 7) return LDM_ERR_ARG;
+  // ksize 2 exists only as the phase form of an upsample conv (upsample == 3)
+  const bool phase = q->upsample == 3;
+  if (phase != (q->ksize == 2)) return LDM_ERR_ARG;
+  if (q->ksize != 1 && q->ksize != 2 && q->ksize != 3 && q->ksize != 5 && q->ksize != 7) return LDM_ERR_ARG;
+  if (phase && (q->stride != 1 || q->c1 || q->pad_mode || q->out_layout != LDM_OUT_NHWC || q->h_out != 2 * q->h_in ||
+                q->w_out != 2 * q->w_in || (q->h_in * q->w_in) % 32 || q->row_stats || q->ln_rows))
+    return LDM_ERR_ARG;
   if (q->act < LDM_ACT_NONE || q->act > LDM_ACT_SIGMOID) return LDM_ERR_ARG;
   if (q->stride != 1 && q->stride != 2) return LDM_ERR_ARG;
-  if (q->upsample < 0 || q->upsample > 2 || (q->upsample && (q->stride != 1))) return LDM_ERR_ARG;
+  if (q->upsample < 0 || q->upsample > 3 || (q->upsample && (q->stride != 1))) return LDM_ERR_ARG;
   if (q->batch <= 0 || q->h_in <= 0 || q->w_in <= 0 || q->h_out <= 0 || q->w_out <= 0) return LDM_ERR_ARG;
   if (q->c0 <= 0 || q->c1 < 0 || (q->c1 > 0 && !q->a1)) return LDM_ERR_ARG;
   if (q->c0 % ce || q->c1 % ce) return LDM_ERR_ALIGN;
@@ -1248,8 +1287,8 @@ int validate(const ldm_conv_params* q, int* es_out) {
   const int pad_sum = q->pad_mode == 1 ? 1 : 2 * (q->ksize / 2);   // total rows/cols of zero padding
   const int hin_eff = q->upsample ? 2 * q->h_in : q->h_in;
   const int win_eff = q->upsample ? 2 * q->w_in : q->w_in;
-  if (q->h_out != (hin_eff + pad_sum - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
-  if (q->w_out != (win_eff + pad_sum - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
+  if (!phase && q->h_out != (hin_eff + pad_sum - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
+  if (!phase && q->w_out != (win_eff + pad_sum - q->ksize) / q->stride + 1) return LDM_ERR_ARG;
   if (q->out_layout == LDM_OUT_GEGLU && (q->n % 32 || q->residual || q->temb || q->gn_partial)) return LDM_ERR_ARG;
   if (q->out_layout == LDM_OUT_SHUFFLE2 && (q->n % 16 || q->temb || q->upsample)) return LDM_ERR_ARG;
   if (q->out_layout < 0 || q->out_layout > 3) return LDM_ERR_ARG;
@@ -1271,7 +1310,7 @@ int validate(const ldm_conv_params* q, int* es_out) {
   }
   const int64_t a0_bytes = (int64_t)q->batch * q->h_in * q->w_in * q->c0 * es;
   const int64_t a1_bytes = (int64_t)q->batch * q->h_in * q->w_in * q->c1 * es;
-  const int64_t w_bytes = (int64_t)q->n * q->kpad * es;
+  const int64_t w_bytes = (int64_t)q->n * q->kpad * es * (phase ? 4 : 1);
   if (M64 >= (1LL << 31) || a0_bytes >= (1LL << 31) - 64 || a1_bytes >= (1LL << 31) - 64 ||
       w_bytes >= (1LL << 31) - 64)
     return LDM_ERR_ARG;  // 32-bit buffer offsets
@@ -1396,7 +1435,7 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
     if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;
   }
 
-  ConvArgs a;
+  ConvArgs a{};
   a.a0 = static_cast<const char*>(q->a0);
   a.a1 = static_cast<const char*>(q->a1);
   a.a0_bytes = (int)((int64_t)q->batch * q->h_in * q->w_in * q->c0 * es);
@@ -1405,8 +1444,10 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.h_in = q->h_in; a.w_in = q->w_in;
   a.h_out = q->h_out; a.w_out = q->w_out; a.hw_out = q->h_out * q->w_out;
   a.ksize = q->ksize; a.stride = q->stride; a.upsample = q->upsample; a.pad = q->pad_mode == 1 ? 0 : q->ksize / 2;
+  a.phase = q->upsample == 3 ? 1 : 0;
+  if (a.phase) { a.upsample = 0; a.pad = 0; }        // taps and offsets come from the phase
   a.w = static_cast<const char*>(q->w);
-  a.w_bytes = (int)((int64_t)q->n * q->kpad * es);
+  a.w_bytes = (int)((int64_t)q->n * q->kpad * es * (a.phase ? 4 : 1));
   a.n = q->n; a.kpad = q->kpad; a.K = q->ksize * q->ksize * cin;
   a.bias = q->bias; a.temb = q->temb; a.temb_stride = q->temb_stride;
   a.residual = static_cast<const char*>(q->residual);

@@ -36,7 +36,20 @@ struct ConvArgs {
   float ln_inv_k, ln_eps;
   int tap_inner;      // K tiles visited channel-block-major, taps inner (see k_state)
   int group_m;        // M panels per raster group (grouped_tile); 1 = plain row-major tiles
+  int phase;          // nearest-2x upsample + 3x3 conv as four 2x2 phase convs (ldm_conv2d upsample 3):
+                      // rows m = (b, phase, y, x) over the low-res grid, W = [4][n][kpad]
 };
+// Storage row of GEMM row m: m itself, or in phase mode (rows ordered (b, phase (dy, dx), y, x) over
+// the h_in x w_in input grid) the output pixel (b, 2y + dy, 2x + dx) of the 2x upsampled image —
+// batch-major either way, so m / hw_out is the batch in both.
+__device__ __forceinline__ int64_t out_row(const ConvArgs& p, int m) {
+  if (!p.phase) return m;
+  const int hwl = p.hw_out >> 2, wl = p.w_out >> 1;
+  const int b = m / p.hw_out, r = m - b * p.hw_out;
+  const int ph = r / hwl, q = r - ph * hwl;
+  const int y = q / wl, x = q - y * wl;
+  return (int64_t)b * p.hw_out + (int64_t)(2 * y + (ph >> 1)) * p.w_out + 2 * x + (ph & 1);
+}
 }  // namespace ldm_igemm
 
 namespace {
@@ -207,7 +220,7 @@ __device__ __forceinline__ void finish4(const ConvArgs& p, int b, int pix, int m
   }
   int64_t idx;
   if (p.out_layout == LDM_OUT_NHWC) {
-    idx = (int64_t)m * N + n;
+    idx = out_row(p, m) * N + n;
     if (p.residual) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += res[r];
@@ -393,7 +406,7 @@ __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0,
         if (q0 + q >= NP || r >= ROWS || m0 + r >= p.M) continue;
         raw(r, c4, v[q]);
         if (nhwc_res) {
-          const int64_t idx = (int64_t)(m0 + r) * N + n;
+          const int64_t idx = out_row(p, m0 + r) * N + n;
           if (n + 3 < N) {
             load4<T>(p.residual, idx, rv[q]);
           } else {
@@ -600,7 +613,7 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
       for (int q = 0; q < GP; ++q) {
         const int r = r0 + (q0 + q) * RP;
         if (res && q0 + q < NP && r < ROWS && m0 + r < p.M)
-          rv[q] = *reinterpret_cast<const uint4*>(res + (int64_t)(m0 + r) * N + n);
+          rv[q] = *reinterpret_cast<const uint4*>(res + out_row(p, m0 + r) * N + n);
       }
 #pragma unroll
       for (int q = 0; q < GP; ++q) {
@@ -638,7 +651,7 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
 #ifdef LDM_ABL_EPI_NO_STORE   // ablation build: the epilogue's math kept, its global stores dropped
         if (packed.x == 0x12345678u && packed.y == 0x9abcdef0u) *reinterpret_cast<uint4*>(out + (int64_t)m * N + n) = packed;
 #else
-        *reinterpret_cast<uint4*>(out + (int64_t)m * N + n) = packed;
+        *reinterpret_cast<uint4*>(out + out_row(p, m) * N + n) = packed;
 #endif
         if (stats) {
           float st[8];

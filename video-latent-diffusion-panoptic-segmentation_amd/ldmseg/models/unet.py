@@ -363,7 +363,7 @@ class UNet(nn.Module):
 
     # ------------------------------------------------------------ packed-weight plan
     def _signature(self):
-        return (self.compute_dtype, self.device, self.ln_fold) + tuple((p.data_ptr(), p._version)
+        return (self.compute_dtype, self.device, self.ln_fold, self.upsample_phases) + tuple((p.data_ptr(), p._version)
                                                                        for p in self.parameters())
 
     @staticmethod
@@ -440,7 +440,12 @@ class UNet(nn.Module):
                                   out=K.PackedConv(a2.to_out[0].weight, a2.to_out[0].bias, dt))
             P[id(t)] = d
         for m in self.modules():
-            if isinstance(m, (Downsample2D, Upsample2D)):
+            if isinstance(m, Upsample2D) and self.upsample_phases:
+                # nearest-2x upsample + 3x3 conv as four 2x2 phase convs over the low-res input
+                # (4/9 of the FLOPs; ldm_conv2d upsample mode 3)
+                # (no src_w: ldm_repack has no phase layout — training runs with the phases off)
+                P[id(m)] = K.PackedConv(m.conv.weight, m.conv.bias, dt, upsample_phases=True)
+            elif isinstance(m, (Downsample2D, Upsample2D)):
                 P[id(m)] = self._pk([m.conv.weight], [m.conv.bias], dt)
         P["out_norm"] = (f32(self.conv_norm_out.weight), f32(self.conv_norm_out.bias))
         P["conv_out"] = self._pk([self.conv_out.weight], [self.conv_out.bias], dt)
@@ -536,6 +541,18 @@ class UNet(nn.Module):
         ldm_feedforward launch (default on; K.feedforward_ok decides per call); off runs the GEGLU
         and ff.net.2 GEMMs separately (A/B — the results are the same bit for bit)."""
         self._ff_fused = bool(enabled)
+
+    @property
+    def upsample_phases(self):
+        return getattr(self, "_up_phases", True)
+
+    def set_upsample_phases(self, enabled=True):
+        """Run every Upsample2D conv as four 2x2 phase convs over its low-res input (default on:
+        4/9 of the 3x3 conv's FLOPs, the taps that read the same source pixel summed in fp32 before
+        the bf16 rounding); off runs the 3x3 conv through the nearest-2x gather (the form the
+        training backward differentiates: LDMTrainStep turns it off with the LayerNorm fold)."""
+        self._up_phases = bool(enabled)
+        self._plan = self._plan_key = self._dplan = None
 
     @property
     def tin_fused(self):

@@ -265,9 +265,25 @@ class PackedConv:
     GEGLU projection in 16-column blocks; ``shuffle2`` packs a ConvTranspose2d(k=2, s=2).
     """
 
-    def __init__(self, weight, bias, dtype, cin_pad=None, geglu=False, shuffle2=False, convt4=False):
+    def __init__(self, weight, bias, dtype, cin_pad=None, geglu=False, shuffle2=False, convt4=False,
+                 upsample_phases=False):
         w = weight.detach()
-        if convt4:
+        self.phases = bool(upsample_phases)
+        if upsample_phases:
+            # conv3x3(nearest_upsample_2x(x)) as four 2x2 convs over x, one per output phase (dy, dx):
+            # out[2y+dy, 2x+dx] = sum_{ty,tx in 0..1} x[y-1+dy+ty, x-1+dx+tx] . Wp[dy,dx][:, :, ty, tx]
+            # with the taps that read the same source pixel summed (in fp32, then rounded once):
+            # rows dy = 0: ty 0 <- ky 0, ty 1 <- ky 1 + 2;  dy = 1: ty 0 <- ky 0 + 1, ty 1 <- ky 2
+            cout, cin, kh, kw = w.shape
+            assert kh == kw == 3, "upsample phases take a 3x3 kernel"
+            wf = w.float()
+            R = torch.tensor([[[1., 0., 0.], [0., 1., 1.]], [[1., 1., 0.], [0., 0., 1.]]], device=w.device)
+            wph = torch.einsum("ayk,bxl,oikl->abyxoi", R, R, wf)      # [dy, dx, ty, tx, cout, cin]
+            wp = wph.permute(0, 1, 4, 2, 3, 5).reshape(4 * cout, 4 * cin)  # rows (dy, dx, co), k (ty, tx, ci)
+            b = None if bias is None else bias.detach().float()
+            self.ksize, self.cin, self.n = 2, cin, cout
+            self.cin_real = cin
+        elif convt4:
             # ConvTranspose2d(k=4, s=2, p=1) weight [cin, cout, 4, 4] as a 3x3 conv (pad 1) with
             # 4 * cout outputs, one per output phase (dy, dx), + the pixel-shuffle epilogue:
             # out[2y+dy, 2x+dx] = sum over taps (ty, tx) of in[y-1+ty, x-1+tx] . W[:, :, ky, kx]
@@ -442,6 +458,8 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
     if x0.dtype != pc.dtype or (x1 is not None and x1.dtype != pc.dtype):
         raise TypeError(f"conv input dtype {x0.dtype} != packed weight dtype {pc.dtype}")
     k = pc.ksize
+    if getattr(pc, "phases", False) and not upsample:
+        raise ValueError("an upsample_phases pack is the nearest-2x upsample conv: pass upsample=True")
     if k == 1:
         ho, wo = h, w
     elif upsample:
@@ -489,7 +507,8 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
         if ln_rows.dtype != torch.float64 or ln_rows.numel() != 2 * M or not ln_rows.is_contiguous():
             raise ValueError("ln rows must be a contiguous fp64 [M, 2] tensor")
         ln_c1, ln_inv_k, ln_eps = pc.ln_c1, 1.0 / (c0 + c1), float(eps)
-    p = ConvParams(_ptr(x0), _ptr(x1), c0, c1, batch, h, w, ho, wo, pc.ksize, stride, int(upsample), _ptr(pc.w),
+    up_mode = 3 if getattr(pc, "phases", False) else int(upsample)
+    p = ConvParams(_ptr(x0), _ptr(x1), c0, c1, batch, h, w, ho, wo, pc.ksize, stride, up_mode, _ptr(pc.w),
                    n, pc.kpad, _ptr(pc.bias), _ptr(temb), temb_stride, _ptr(residual), _ptr(out), out_layout, act,
                    dtype_code(pc.dtype), int(odt == torch.float32 and pc.dtype != torch.float32), None, 0,
                    _ptr(part), int(pad_mode), unit, slots, _ptr(row_stats), _ptr(ln_rows), _ptr(ln_c1),

@@ -90,7 +90,9 @@ class LDMTrainStep:
         # plain layout of its parameters, refreshed in place after each update (models/repack.py).
         # The module's inference setting is restored inside ``for_inference()`` (validation sampling)
         self._inference_fold = unet.ln_fold
+        self._inference_phases = unet.upsample_phases
         unet.set_ln_fold(False)
+        unet.set_upsample_phases(False)           # the backward differentiates the 3x3 upsample conv
         self.refresher = PackRefresher(unet)
         self.self_condition = self_condition
         self.min_noise_level = min_noise_level
@@ -334,10 +336,12 @@ class LDMTrainStep:
         The packs are rebuilt for the folded plan on entry and for the training plan on exit
         (one prepare() each way)."""
         self.unet.set_ln_fold(self._inference_fold)
+        self.unet.set_upsample_phases(self._inference_phases)
         try:
             yield self.unet
         finally:
             self.unet.set_ln_fold(False)
+            self.unet.set_upsample_phases(False)
 
     def _sink(self, p):
         return self.flat.view_of(p, self.flat.grad), False
@@ -348,6 +352,8 @@ class LDMTrainStep:
         u, sch = self.unet, self.sched
         if u.ln_fold:                                       # re-enabled by the caller since construction
             u.set_ln_fold(False)
+        if u.upsample_phases:
+            u.set_upsample_phases(False)
         B = latents.shape[0]
         dev = latents.device
         if noise is None:
