@@ -233,6 +233,9 @@ void ldm_attention_force_legacy(int legacy);
 /* Tuning / A-B hook: 1 (default) runs head_dim 80 on the 32x32x16 kernel of head_dim 40, 0 on the
  * 16x16x32 one. */
 void ldm_attention_set_d80(int enabled);
+/* tuning / A-B hook: head_dim 40 with 64 queries per wave (two 32-query subtiles sharing every
+ * K / V fragment read; 8 waves, one block per CU) */
+void ldm_attention_set_qs2(int enabled);
 /* Tuning / A-B hook: 1 (default) runs the bf16 backward for head_dim <= 64 on the 32x32x16 MFMA
  * kernels, 0 on the 16x16x16 ones. */
 void ldm_attention_set_bwd32(int enabled);

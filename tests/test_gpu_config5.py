@@ -99,6 +99,53 @@ def test_fp8_scaled_attention_d40(N, B):
     assert l2 <= 6e-2
 
 
+@pytest.mark.parametrize("qs,ks,vs", [(1.0, 1.0, 1.0), (5e-3, 200.0, 1.0), (1e3, 1e-3, 1.0), (1.0, 1.0, 1e3),
+                                      (1.0, 1.0, 1e-2), (1e-2, 1e-2, 1e-2), (1e-3, 1e3, 5e2)])
+def test_fp8_scaled_attention_d40_magnitudes(qs, ks, vs):
+    """The block-scaled kernel's per-32-element E8M0 scales against operand magnitude: Q, K, V
+    scaled by (qs, ks, vs).  qs ks = 1 leaves the scores as in the unit case while K (or Q) moves
+    far past e4m3's 448 and Q (or K) deep into its subnormals — unit scales clip / flush them
+    (the scales are what keeps this path correct); V at 1e3 / 1e-2 likewise; (1e-2, 1e-2, 1e-2) is
+    a flat softmax over small values.  Same bar as the unit-magnitude case: rel-L2 <= 6e-2."""
+    C, heads, B, N = 320, 8, 2, 2048
+    g = torch.Generator(device=DEV).manual_seed(11)
+    base = torch.randn(B, N, 3, C, device=DEV, generator=g)
+    base = base * torch.tensor([qs, ks, vs], device=DEV).view(1, 1, 3, 1)
+    qkv = base.reshape(B, N, 3 * C).to(torch.bfloat16)
+    x = qkv.float().view(B, N, 3, heads, 40).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(x[0] @ x[1].transpose(-1, -2) * 40 ** -0.5, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B, N, C)
+    out = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, 40, N, N, 3 * C, 3 * C, 3 * C, fp8=True)
+    l2 = ((out.float() - ref).norm() / ref.norm()).item()
+    print(f"scales q {qs:g} k {ks:g} v {vs:g}: fp8 rel-L2 {l2:.3e}")
+    assert torch.isfinite(out.float()).all()
+    assert l2 <= 6e-2
+
+
+@pytest.mark.parametrize("N,B", [(2048, 8), (2048 + 29, 8)])
+def test_fp8_scaled_attention_d40_qs2(N, B):
+    """The block-scaled kernel with two 32-query subtiles per wave (ldm_attention_set_qs2; used when
+    it gives >= 256 blocks): same bar as the one-subtile form against torch fp32 (rel-L2 <= 6e-2),
+    and within e4m3 rounding of it."""
+    C, heads = 320, 8
+    g = torch.Generator(device=DEV).manual_seed(N + 1)
+    qkv = torch.randn(B, N, 3 * C, device=DEV, generator=g).to(torch.bfloat16)
+    x = qkv.float().view(B, N, 3, heads, 40).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(x[0] @ x[1].transpose(-1, -2) * 40 ** -0.5, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B, N, C)
+    outs = []
+    try:
+        for on in (False, True):
+            K.set_attention_qs2(on)
+            outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, heads, 40, N, N, 3 * C, 3 * C, 3 * C,
+                                    fp8=True).float())
+    finally:
+        K.set_attention_qs2(False)
+    for o in outs:
+        l2 = ((o - ref).norm() / ref.norm()).item()
+        print(f"N={N} B={B}: fp8 rel-L2 {l2:.3e}")
+        assert torch.isfinite(o).all() and l2 <= 6e-2
+    assert ((outs[0] - outs[1]).norm() / ref.norm()).item() < 3e-2
+
+
 def test_unet_config5_fp8_attention_close_to_oracle():
     """The config-5 UNet at T=16, 32x64 latents with fp8 P.V in every self-attention: frames 0
     and 15 against the fp32 oracle, bar 1.2e-1 (bf16 compute + e4m3 P.V, see the op test)."""

@@ -313,6 +313,30 @@ def test_attention_d80_forms_agree(B, N):
     assert torch.allclose(outs[0][1], outs[1][1], atol=2e-2)
 
 
+@pytest.mark.parametrize("B,N", [(4, 4096), (4, 4096 + 37)])
+def test_attention_d40_qs2_close_to_default(B, N):
+    """head_dim 40 with two 32-query subtiles per wave (ldm_attention_set_qs2) against the default
+    one-subtile kernel and a torch fp32 reference on the device: within the bf16 bar, and within
+    bf16 rounding of each other (the shared rescale decision moves m by different bf16 steps, so
+    not bit-identical); a ragged N exercises the masked last key tile and the partial query block."""
+    torch.manual_seed(9)
+    C, H = 320, 8
+    qkv = torch.randn(B, N, 3 * C, device=DEV).to(torch.bfloat16)
+    x = qkv.float().view(B, N, 3, H, 40).permute(2, 0, 3, 1, 4)
+    ref = torch.cat([torch.softmax(x[0][b:b + 1] @ x[1][b:b + 1].transpose(-1, -2) * 40 ** -0.5, -1) @ x[2][b:b + 1]
+                     for b in range(B)]).permute(0, 2, 1, 3).reshape(B, N, C)
+    outs = []
+    try:
+        for on in (False, True):
+            K.set_attention_qs2(on)
+            outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, 40, N, N, 3 * C, 3 * C, 3 * C).float())
+    finally:
+        K.set_attention_qs2(False)
+    for o in outs:
+        assert ((o - ref).norm() / ref.norm()).item() < 1e-2
+    assert (outs[0] - outs[1]).abs().max().item() < 0.05
+
+
 def test_attention_softmax_spike():
     """Force the online-softmax rescale: a huge logit in the LAST kv tile of some rows."""
     torch.manual_seed(4)

@@ -682,11 +682,12 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 // level).  Q.K^T runs over DQ = D + 1 (the max column) rounded up to 16 (48 / 96: 3 / 6 MFMAs per
 // 32-key block), P.V over ND32 = ceil((D + 1) / 32) 32-row head-dim blocks (2 / 3, the ones column
 // d = D carrying the denominator).
-template <int NW, int OCC, int KT = 64, int D = 40>
+template <int NW, int OCC, int KT = 64, int D = 40, int QS = 1>
 __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p) {
   typedef bf16_t T;
   typedef __attribute__((ext_vector_type(16))) float f32x16_t;
   static_assert(D % 8 == 0, "head dim");
+  static_assert(QS == 1 || (QS == 2 && KT == 64), "query subtiles");
   constexpr int DQ = (D + 16) / 16 * 16, QC = DQ / 16, ND32 = (D + 32) / 32;
   constexpr int EPC = 8, CPR = (DQ > 32 * ND32 ? DQ : 32 * ND32) / 8, RCH = CPR + 1, ROW = RCH * EPC,
                 TILE = KT * ROW, ES = 2;
@@ -699,7 +700,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   const int r32 = lane & 31, hh = lane >> 5, i16 = lane & 15;
   int qb, h, b;
   {
-    const int nqb = (p.nq + 32 * NW - 1) / (32 * NW);
+    const int nqb = (p.nq + 32 * QS * NW - 1) / (32 * QS * NW);
     const int bid = blockIdx.x, nblk = gridDim.x;
     const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
     const int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
@@ -708,7 +709,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
     h = hb % p.heads;
     b = hb / p.heads;
   }
-  const int qbase = qb * (32 * NW) + wave * 32;
+  // a wave owns QS subtiles of 32 queries: qbase + 32 s + r32
+  const int qbase = qb * (32 * QS * NW) + wave * (32 * QS);
   const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
   const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
   const T* vp = reinterpret_cast<const T*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * p.d;
@@ -771,94 +773,123 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   };
   const float c2 = p.scale_log2;
 
-  // Q^T (B operand) chunk c: lane holds Q[q = qbase + r32][d = 16c + 8hh .. +8] * c2; the max
-  // column d = D is element 0 of chunk D / 16 in the hh = (D % 16) / 8 lanes (initially -m = 0)
-  uint4 qf[QC];
-  {
-    const int qi = qbase + r32;
+  // Q^T (B operand) chunk c of subtile s: lane holds Q[q = qbase + 32 s + r32][d = 16c + 8hh .. +8]
+  // * c2; the max column d = D is element 0 of chunk D / 16 in the hh = (D % 16) / 8 lanes
+  // (initially -m = 0)
+  uint4 qf[QS][QC];
+#pragma unroll
+  for (int s = 0; s < QS; ++s) {
+    const int qi = qbase + 32 * s + r32;
     const T* qrow = qp + (int64_t)qi * p.qs;
 #pragma unroll
     for (int c = 0; c < QC; ++c) {
       const int dd = 16 * c + 8 * hh;
-      if (qi < p.nq && dd < p.d) qf[c] = scale_bf16x8(*reinterpret_cast<const uint4*>(qrow + dd), c2);
-      else qf[c] = make_uint4(0u, 0u, 0u, 0u);
+      if (qi < p.nq && dd < p.d) qf[s][c] = scale_bf16x8(*reinterpret_cast<const uint4*>(qrow + dd), c2);
+      else qf[s][c] = make_uint4(0u, 0u, 0u, 0u);
     }
   }
-  f32x16_t oacc[ND32];
+  f32x16_t oacc[QS][ND32];
 #pragma unroll
-  for (int db = 0; db < ND32; ++db)
+  for (int s = 0; s < QS; ++s)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) oacc[db][r] = 0.f;
-  float mq = 0.f;
+    for (int db = 0; db < ND32; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[s][db][r] = 0.f;
+  float mq[QS];
+#pragma unroll
+  for (int s = 0; s < QS; ++s) mq[s] = 0.f;
 
   typedef __attribute__((ext_vector_type(4))) short s4_t;
   typedef __attribute__((address_space(3))) s4_t lds_s4_t;
-  auto compute = [&](int buf, int kv0, bool masked, bool first, int half) {
-    const T* Ks = lds + buf * 2 * TILE + half * 64 * ROW;
-    const T* Vs = lds + buf * 2 * TILE + TILE + half * 64 * ROW;
-    kv0 += 64 * half;
-    first = first && half == 0;
-    f32x16_t sacc[2];
+  // the lane's max over a subtile's 64 scores of this tile (a tree of max3, then the other half)
+  auto tile_max = [&](const f32x16_t (&sa)[2]) {
+    float t[11];
 #pragma unroll
-    for (int blk = 0; blk < 2; ++blk) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[blk][r] = 0.f;
-      const T* krow = Ks + (32 * blk + r32) * ROW + 8 * hh;
-#pragma unroll
-      for (int c = 0; c < QC; ++c) {
-        const uint4 ka = *reinterpret_cast<const uint4*>(krow + 16 * c);
-        sacc[blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, ka),
-                                                            __builtin_bit_cast(bf16x8_t, qf[c]), sacc[blk], 0, 0, 0);
-      }
+    for (int k = 0; k < 10; ++k) {
+      const int a = 3 * k;
+      t[k] = vmax3(a < 16 ? sa[0][a] : sa[1][a - 16], a + 1 < 16 ? sa[0][a + 1] : sa[1][a + 1 - 16],
+                   a + 2 < 16 ? sa[0][a + 2] : sa[1][a + 2 - 16]);
     }
-    if (masked) {
-#pragma unroll
-      for (int blk = 0; blk < 2; ++blk)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kv0 + 32 * blk + 8 * (r >> 2) + 4 * hh + (r & 3) >= p.nkv) sacc[blk][r] = -INFINITY;
-    }
-    float mx;
-    {
-      float t[11];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        const int a = 3 * k;
-        t[k] = vmax3(a < 16 ? sacc[0][a] : sacc[1][a - 16], a + 1 < 16 ? sacc[0][a + 1] : sacc[1][a + 1 - 16],
-                     a + 2 < 16 ? sacc[0][a + 2] : sacc[1][a + 2 - 16]);
-      }
-      t[10] = __builtin_elementwise_maximum(sacc[1][14], sacc[1][15]);
-      const float u0 = vmax3(t[0], t[1], t[2]), u1 = vmax3(t[3], t[4], t[5]), u2 = vmax3(t[6], t[7], t[8]);
-      mx = vmax3(vmax3(u0, u1, u2), t[9], t[10]);
-      unsigned w = __float_as_uint(mx);
-      const auto sw = __builtin_amdgcn_permlane32_swap(w, w, false, false);
-      mx = vmax3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), mx);
-    }
-    // accumulators are s * c2 - m already; the first tile always sets m (from m = 0)
-    if (first || __any(mx > kRescaleThr)) {
-      const float tgt = mq + mx;
-      const float mn = bf16_rne(first ? tgt : fmaxf(mq, tgt));
-      const float delta = mn - mq;
-      const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);   // (O = 0 on the first tile)
-      mq = mn;
-#pragma unroll
-      for (int db = 0; db < ND32; ++db) oacc[db] *= alpha;
-      sacc[0] -= delta;
-      sacc[1] -= delta;
-      if (hh == (D % 16) / 8) qf[D / 16].x = (qf[D / 16].x & 0xffff0000u) | (__float_as_uint(-mn) >> 16);
-    }
-    uint4 pb[2][2];                           // bf16 P^T fragment of k-step (block, s)
+    t[10] = __builtin_elementwise_maximum(sa[1][14], sa[1][15]);
+    const float u0 = vmax3(t[0], t[1], t[2]), u1 = vmax3(t[3], t[4], t[5]), u2 = vmax3(t[6], t[7], t[8]);
+    float mx = vmax3(vmax3(u0, u1, u2), t[9], t[10]);
+    unsigned w = __float_as_uint(mx);
+    const auto sw = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+    return vmax3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), mx);
+  };
+  auto to_p = [&](const f32x16_t (&sa)[2], uint4 (&pb)[2][2]) {   // bf16 P^T fragments of k-step (blk, st)
 #pragma unroll
     for (int blk = 0; blk < 2; ++blk)
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
         float pv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pv[j] = __builtin_amdgcn_exp2f(sacc[blk][8 * st + j]);
+        for (int j = 0; j < 8; ++j) pv[j] = __builtin_amdgcn_exp2f(sa[blk][8 * st + j]);
         pb[blk][st] = make_uint4(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]), pack_bf16x2(pv[4], pv[5]),
                                  pack_bf16x2(pv[6], pv[7]));
       }
-    // O^T += V^T P^T: A = V^T rows d (block db) for keys 16s' + {4hh..+3, 8 + 4hh..+3} of block blk
+  };
+  auto compute = [&](int buf, int kv0, bool masked, bool first, int half) {
+    const T* Ks = lds + buf * 2 * TILE + half * 64 * ROW;
+    const T* Vs = lds + buf * 2 * TILE + TILE + half * 64 * ROW;
+    kv0 += 64 * half;
+    first = first && half == 0;
+    f32x16_t sacc[QS][2];
+    // S^T = K Q^T: each K fragment read from LDS feeds the MFMAs of every subtile
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+      for (int s = 0; s < QS; ++s)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[s][blk][r] = 0.f;
+      const T* krow = Ks + (32 * blk + r32) * ROW + 8 * hh;
+#pragma unroll
+      for (int c = 0; c < QC; ++c) {
+        const uint4 ka = *reinterpret_cast<const uint4*>(krow + 16 * c);
+#pragma unroll
+        for (int s = 0; s < QS; ++s)
+          sacc[s][blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, ka),
+                                                                 __builtin_bit_cast(bf16x8_t, qf[s][c]), sacc[s][blk], 0, 0, 0);
+      }
+    }
+    if (masked) {
+#pragma unroll
+      for (int s = 0; s < QS; ++s)
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * blk + 8 * (r >> 2) + 4 * hh + (r & 3) >= p.nkv) sacc[s][blk][r] = -INFINITY;
+    }
+    float mx[QS];
+    bool resc = first;
+#pragma unroll
+    for (int s = 0; s < QS; ++s) {
+      mx[s] = tile_max(sacc[s]);
+      resc = resc || mx[s] > kRescaleThr;
+    }
+    // accumulators are s * c2 - m already; the first tile always sets m (from m = 0).  One wave-
+    // uniform branch for all subtiles (a subtile rescaled without need only moves m up to its max)
+    if (first || __any(resc)) {
+#pragma unroll
+      for (int s = 0; s < QS; ++s) {
+        const float tgt = mq[s] + mx[s];
+        const float mn = bf16_rne(first ? tgt : fmaxf(mq[s], tgt));
+        const float delta = mn - mq[s];
+        const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);   // (O = 0 on the first tile)
+        mq[s] = mn;
+#pragma unroll
+        for (int db = 0; db < ND32; ++db) oacc[s][db] *= alpha;
+        sacc[s][0] -= delta;
+        sacc[s][1] -= delta;
+        if (hh == (D % 16) / 8) qf[s][D / 16].x = (qf[s][D / 16].x & 0xffff0000u) | (__float_as_uint(-mn) >> 16);
+      }
+    }
+    uint4 pb[QS][2][2];
+#pragma unroll
+    for (int s = 0; s < QS; ++s) to_p(sacc[s], pb[s]);
+    // O^T += V^T P^T: A = V^T rows d (block db) for keys 16s' + {4hh..+3, 8 + 4hh..+3} of block blk;
+    // each V fragment feeds every subtile
 #pragma unroll
     for (int db = 0; db < ND32; ++db) {
       const int cb = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
@@ -870,8 +901,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
           const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0)));
           const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0 + 8 * ROW)));
           const uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
-          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, va),
-                                                             __builtin_bit_cast(bf16x8_t, pb[blk][st]), oacc[db], 0, 0, 0);
+#pragma unroll
+          for (int s = 0; s < QS; ++s)
+            oacc[s][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, va),
+                                                                  __builtin_bit_cast(bf16x8_t, pb[s][blk][st]), oacc[s][db], 0, 0, 0);
         }
     }
   };
@@ -896,22 +929,25 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   // denominator: O^T row d = D = block D / 32, register 4 ((D % 32) / 8) of the hh = 0 lane of this
   // column (a 32x32 result row 8 (r >> 2) + 4 hh + (r & 3) sits in register r of the hh half)
   static_assert(D % 8 == 0, "denominator row");
-  const float lt = __shfl(oacc[D / 32][4 * ((D % 32) / 8)], r32, 64);
-  const float inv = 1.0f / lt;
-  const int qi = qbase + r32;
-  if (qi < p.nq) {
-    if (p.lse && hh == 0) p.lse[((int64_t)b * p.heads + h) * p.nq + qi] = mq + __log2f(lt);
-    T* orow = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * p.d + (int64_t)qi * p.os;
 #pragma unroll
-    for (int db = 0; db < ND32; ++db)
+  for (int s = 0; s < QS; ++s) {
+    const float lt = __shfl(oacc[s][D / 32][4 * ((D % 32) / 8)], r32, 64);
+    const float inv = 1.0f / lt;
+    const int qi = qbase + 32 * s + r32;
+    if (qi < p.nq) {
+      if (p.lse && hh == 0) p.lse[((int64_t)b * p.heads + h) * p.nq + qi] = mq[s] + __log2f(lt);
+      T* orow = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * p.d + (int64_t)qi * p.os;
 #pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4) {
-        const int d = 32 * db + 8 * g4 + 4 * hh;
-        if (32 * db + 8 * g4 >= D) break;          // (compile-time: D % 8 == 0)
-        *reinterpret_cast<uint2*>(orow + d) =
-            make_uint2(pack_bf16x2(oacc[db][4 * g4] * inv, oacc[db][4 * g4 + 1] * inv),
-                       pack_bf16x2(oacc[db][4 * g4 + 2] * inv, oacc[db][4 * g4 + 3] * inv));
-      }
+      for (int db = 0; db < ND32; ++db)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = 32 * db + 8 * g4 + 4 * hh;
+          if (32 * db + 8 * g4 >= D) break;          // (compile-time: D % 8 == 0)
+          *reinterpret_cast<uint2*>(orow + d) =
+              make_uint2(pack_bf16x2(oacc[s][db][4 * g4] * inv, oacc[s][db][4 * g4 + 1] * inv),
+                         pack_bf16x2(oacc[s][db][4 * g4 + 2] * inv, oacc[s][db][4 * g4 + 3] * inv));
+        }
+    }
   }
 }
 
@@ -961,6 +997,7 @@ int launch32_dp_mc(const AttnArgs& a, int batch, hipStream_t s) {
 }
 
 int g_attn_d80 = 1;      // tuning / A-B hook: 0 routes head_dim 80 to the 16x16x32 kernel
+int g_attn_qs2 = 0;      // tuning / A-B hook: 1 runs head_dim 40 as 64 queries per wave (two subtiles)
 
 template <int DP, bool F8 = false>
 int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
@@ -983,7 +1020,11 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
       const int nblk = (a.nq + 255) / 256 * a.heads * batch;
       // (measured at N=4096: 8 waves x 2 blocks per CU 241 us; 4 waves x 4 blocks 302 us — each K/V
       // tile then serves half the queries; 128-key tiles 249 us)
-      if (g_attn_waves == 4) {
+      const int nb2 = (a.nq + 511) / 512 * a.heads * batch;
+      if (g_attn_qs2 && g_attn_waves == 0 && nb2 >= 256) {
+        // 8 waves x 64 queries (two subtiles sharing every K / V fragment read), one block per CU
+        hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 40, 2>), dim3(nb2), dim3(512), 0, s, a);
+      } else if (g_attn_waves == 4) {
         const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
         hipLaunchKernelGGL((attn_d40_kernel<4, 4>), dim3(nb4), dim3(256), 0, s, a);
       } else if (nblk >= 512 || g_attn_waves == 8) hipLaunchKernelGGL((attn_d40_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a);
@@ -1003,12 +1044,15 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
 
 // ======================================================================================
 // fp8 attention at head_dim 40 (BASELINE config 5's 32x64 level, N = 2048) on the block-scaled
-// v_mfma_scale_f32_32x32x64_f8f6f4 with e4m3 operands and unit (E8M0 127) scales: twice the bf16
-// MFMA rate per clock, and a 64-deep K per instruction, so per 64-key tile and wave
+// v_mfma_scale_f32_32x32x64_f8f6f4 with e4m3 operands: twice the bf16 MFMA rate per clock, and a
+// 64-deep K per instruction, so per 64-key tile and wave
 //   S^T = K Q^T      2 MFMAs (one per 32-key block; d = 40 + the max column padded to 64)
 //   O^T += V^T P^T   2 MFMAs (one per 32-row head-dim block, all 64 keys at once)
-// against 6 + 8 x 32x32x16 bf16 issues (attn_d40_kernel).  e4m3's range (2^-9 .. 448) holds
-// Q * scale * log2(e), K, V and P (<= 2^8 under the lazy rescale) without per-block scaling.
+// against 6 + 8 x 32x32x16 bf16 issues (attn_d40_kernel).  Every 32-element operand block carries
+// its own E8M0 scale (the instruction's per-lane scale operands, free): K per (key, d half), V^T
+// per (d, key half), Q per (query, d half), chosen so the block's max lands in [224, 448] — no
+// clipping of large activations and no subnormal collapse of small ones (f8_block_exp).  P keeps
+// the unit scale (P' <= 2^8 under the lazy rescale).
 // K and V are quantized once per call by attn_f8_prep into 4-KB LDS images per 64-key tile (K8:
 // [key][64 B] with d = 40 set to 1.0; V8T: [d][64 keys in the P.V k order] with row 40 = 1.0,
 // the softmax denominator), 16-byte chunks XOR-swizzled so every ds_read_b128 is conflict-free;
@@ -1026,15 +1070,34 @@ __device__ __forceinline__ int f8_swz(int row, int c) { return c ^ ((row >> 2) &
 __device__ __forceinline__ int f8_pv_key(int kb, int j) { return 32 * (j >> 4) + 8 * ((j >> 2) & 3) + 4 * kb + (j & 3); }
 __device__ __forceinline__ float bf16_bits_f(unsigned short u) { return __uint_as_float((unsigned)u << 16); }
 
-// grid (ceil(nkv / 64), heads, batch), 256 threads: one K8 and one V8T image per 64-key tile
+// E8M0 exponent e (scale 2^e) for a 32-element block with max |x| = amax: the smallest e with
+// amax 2^-e <= 448 (e4m3's max), so the block's largest value lands in [224, 448] and the rest keep
+// e4m3's relative precision down to 2^-6 of it before going subnormal; clamped to [lo, hi]
+__device__ __forceinline__ int f8_block_exp(float amax, int lo, int hi) {
+  int e = 0;
+  if (amax > 0.f) {
+    int ex;
+    const float m = frexpf(amax * (1.f / 448.f), &ex);
+    e = m > 0.5f ? ex : ex - 1;
+  }
+  return min(max(e, lo), hi);
+}
+
+// grid (ceil(nkv / 64), heads, batch), 256 threads: one K8 and one V8T image per 64-key tile, the
+// tile's 256 E8M0 scale bytes (sc: [lane][4], byte i of lane (hh, r32) = K rows 32 i + r32 for
+// i < 2, V^T rows 32 (i - 2) + r32 for i >= 2, each over that lane's 32-element k half hh), and
+// max |K| of the (batch, head) into kmax (atomic; zeroed by the launcher)
 __global__ __launch_bounds__(256) void attn_f8_prep(const AttnArgs p, uint8_t* __restrict__ k8,
-                                                    uint8_t* __restrict__ v8t) {
+                                                    uint8_t* __restrict__ v8t, uint8_t* __restrict__ sc,
+                                                    unsigned* __restrict__ kmax) {
   __shared__ unsigned short vs[64][66];
   const int t = blockIdx.x, h = blockIdx.y, b = blockIdx.z, ntile = gridDim.x, tid = threadIdx.x;
   const int hd = p.d;
   const unsigned short* kp = reinterpret_cast<const unsigned short*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * hd;
   const unsigned short* vp = reinterpret_cast<const unsigned short*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * hd;
-  const int64_t img = (((int64_t)b * p.heads + h) * ntile + t) * F8_IMG;
+  const int64_t tile = ((int64_t)b * p.heads + h) * ntile + t;
+  const int64_t img = tile * F8_IMG;
+  uint8_t* const scale = sc + tile * 256;
   // V tile -> LDS (bf16 bits, zero past nkv / hd)
   for (int i = tid; i < 64 * 8; i += 256) {
     const int key = i >> 3, c = i & 7, k = t * 64 + key;
@@ -1044,10 +1107,11 @@ __global__ __launch_bounds__(256) void attn_f8_prep(const AttnArgs p, uint8_t* _
 #pragma unroll
     for (int j = 0; j < 8; ++j) vs[key][8 * c + j] = e[j];
   }
-  // K8: row r, chunk c = d 16c .. 16c + 15
+  // K8: row r, chunk c = d 16c .. 16c + 15; chunks 2 hh, 2 hh + 1 (threads c, c ^ 1) form one block
   {
     const int r = tid >> 2, c = tid & 3, k = t * 64 + r;
     float f[16];
+    float amax = 0.f, kabs = 0.f;
 #pragma unroll
     for (int hv = 0; hv < 2; ++hv) {
       const int d0 = 16 * c + 8 * hv;
@@ -1055,35 +1119,58 @@ __global__ __launch_bounds__(256) void attn_f8_prep(const AttnArgs p, uint8_t* _
       if (k < p.nkv && d0 < hd) v = *reinterpret_cast<const uint4*>(kp + (int64_t)k * p.ks + d0);
       const unsigned short* e = reinterpret_cast<const unsigned short*>(&v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[8 * hv + j] = (d0 + j == hd && k < p.nkv) ? 1.f : sat448(bf16_bits_f(e[j]));
+      for (int j = 0; j < 8; ++j) {
+        const float x = bf16_bits_f(e[j]);
+        kabs = fmaxf(kabs, fabsf(x));
+        f[8 * hv + j] = (d0 + j == hd && k < p.nkv) ? 1.f : x;
+      }
     }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(f[j]));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    // the max-column block (d 32 .. 63 holds d = 40 = 1.0) keeps 2^-e inside e4m3: e in [-8, 9]
+    const int e = c >= 2 ? f8_block_exp(amax, -8, 9) : f8_block_exp(amax, -100, 100);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) f[j] = sat448(ldexpf(f[j], -e));
     const uint4 w = make_uint4(pack_fp8x4(f[0], f[1], f[2], f[3]), pack_fp8x4(f[4], f[5], f[6], f[7]),
                                pack_fp8x4(f[8], f[9], f[10], f[11]), pack_fp8x4(f[12], f[13], f[14], f[15]));
     *reinterpret_cast<uint4*>(k8 + img + r * 64 + f8_swz(r, c) * 16) = w;
+    if ((c & 1) == 0) scale[((c >> 1) * 32 + (r & 31)) * 4 + (r >> 5)] = (uint8_t)(e + 127);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) kabs = fmaxf(kabs, __shfl_xor(kabs, o, 64));
+    if ((tid & 63) == 0) atomicMax(kmax + (int64_t)b * p.heads + h, __float_as_uint(kabs));
   }
   __syncthreads();
   // V8T: row dr (head-dim index), chunk c = k-order positions 16c .. 16c + 15 (lane half kb = c >> 1)
   {
     const int dr = tid >> 2, c = tid & 3, kb = c >> 1;
     float f[16];
+    float amax = 0.f;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int key = f8_pv_key(kb, 16 * (c & 1) + j);
       float x = 0.f;
-      if (dr < hd) x = sat448(bf16_bits_f(vs[key][dr]));
+      if (dr < hd) x = bf16_bits_f(vs[key][dr]);
       else if (dr == hd) x = 1.f;
       f[j] = x;
+      amax = fmaxf(amax, fabsf(x));
     }
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    const int e = f8_block_exp(amax, -100, 100);   // the ones row: e = -8, 2^8 exact
+#pragma unroll
+    for (int j = 0; j < 16; ++j) f[j] = sat448(ldexpf(f[j], -e));
     const uint4 w = make_uint4(pack_fp8x4(f[0], f[1], f[2], f[3]), pack_fp8x4(f[4], f[5], f[6], f[7]),
                                pack_fp8x4(f[8], f[9], f[10], f[11]), pack_fp8x4(f[12], f[13], f[14], f[15]));
     *reinterpret_cast<uint4*>(v8t + img + dr * 64 + f8_swz(dr, c) * 16) = w;
+    if ((c & 1) == 0) scale[(kb * 32 + (dr & 31)) * 4 + 2 + (dr >> 5)] = (uint8_t)(e + 127);
   }
 }
 
 typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 
-__device__ __forceinline__ f32x16_t mma_f8(const i32x8_t a, const i32x8_t b, f32x16_t c, int e8_one) {
-  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, e8_one, 0, e8_one);
+// the lane's E8M0 scale bytes: sa for its A row block, sb for its B column block
+__device__ __forceinline__ f32x16_t mma_f8(const i32x8_t a, const i32x8_t b, f32x16_t c, int sa, int sb) {
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
 }
 
 // a lane's 32 bytes (chunks 2 hh, 2 hh + 1) of row `row` of a swizzled 64-byte-row image
@@ -1098,9 +1185,11 @@ __device__ __forceinline__ i32x8_t f8_row32(const uint8_t* img, int row, int hh)
 
 __device__ __forceinline__ float fp8_to_f(int byte) { return __builtin_amdgcn_cvt_f32_fp8(byte, 0); }
 
-template <int NW, int OCC>
+template <int NW, int OCC, int QS = 1>
 __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p, const uint8_t* __restrict__ k8,
-                                                              const uint8_t* __restrict__ v8t, int e8_one) {
+                                                              const uint8_t* __restrict__ v8t,
+                                                              const unsigned* __restrict__ sc,
+                                                              const float* __restrict__ kmax, int e8_one) {
   constexpr int HD = 40;                       // head_dim (the max / ones column)
   __shared__ uint4 smem[2 * 2 * F8_IMG / 16];  // [buf][K8 | V8T]
   const uint8_t* const lds = reinterpret_cast<const uint8_t*>(smem);
@@ -1110,7 +1199,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
   const int r32 = lane & 31, hh = lane >> 5;
   int qb, h, b;
   {
-    const int nqb = (p.nq + 32 * NW - 1) / (32 * NW);
+    const int nqb = (p.nq + 32 * QS * NW - 1) / (32 * QS * NW);
     const int bid = blockIdx.x, nblk = gridDim.x;
     const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
     const int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
@@ -1119,10 +1208,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
     h = hb % p.heads;
     b = hb / p.heads;
   }
-  const int qbase = qb * (32 * NW) + wave * 32;
+  const int qbase = qb * (32 * QS * NW) + wave * (32 * QS);   // subtile s: queries qbase + 32 s + r32
   const int ntiles = (p.nkv + 63) / 64;
   const uint8_t* kimg = k8 + (((int64_t)b * p.heads + h) * ntiles) * F8_IMG;
   const uint8_t* vimg = v8t + (((int64_t)b * p.heads + h) * ntiles) * F8_IMG;
+  const unsigned* scl = sc + (((int64_t)b * p.heads + h) * ntiles) * 64 + lane;   // [tile][lane] dwords
 
   auto issue_tile = [&](int t, int buf) {     // 8 x 1 KB: K8 then V8T
     for (int i = wave; i < 8; i += NW) {
@@ -1132,143 +1222,216 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
     }
   };
 
-  // Q (B operand): lane holds Q[q = qbase + r32][d = 32 hh + j] * scale * log2(e) as e4m3, j < 32;
-  // d = 40 (hh = 1, byte 8 = dword 2 byte 0) carries -m
+  // Q (B operand): lane holds Q[q = qbase + 32 s + r32][d = 32 hh + j] * scale * log2(e) / 2^eq as
+  // e4m3, j < 32, its E8M0 scale eq + 127 in qsc; d = 40 (hh = 1, byte 8 = dword 2 byte 0) carries
+  // -m / 2^eq1.  eq1 (the hh = 1 block) also covers every m the loop can reach: |m| <= max |s c| + 6
+  // <= |q c|_1 max |K| + 6 (+ 1/8 for the e4m3 rounding of q and k), so -m never saturates.
   const float c2 = p.scale_log2;
-  i32x8_t qf;
-  {
-    const int qi = qbase + r32;
+  const float kmx = kmax[(int64_t)b * p.heads + h];
+  i32x8_t qf[QS];
+  int qsc[QS];
+  float m_up[QS], m_dn[QS];                    // 2^eq1, 2^-eq1 (the max column's scale, both lane halves)
+#pragma unroll
+  for (int s = 0; s < QS; ++s) {
+    const int qi = qbase + 32 * s + r32;
     const bf16_t* qrow = reinterpret_cast<const bf16_t*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * HD +
                          (int64_t)qi * p.qs;
+    float f[32];
+    float amax = 0.f, l1 = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {             // 8 d-values per 16-byte chunk
       const int d0 = 32 * hh + 8 * c;
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (qi < p.nq && d0 < HD) v = *reinterpret_cast<const uint4*>(qrow + d0);
-      const float f0 = __uint_as_float(v.x << 16) * c2, f1 = __uint_as_float(v.x & 0xffff0000u) * c2;
-      const float f2 = __uint_as_float(v.y << 16) * c2, f3 = __uint_as_float(v.y & 0xffff0000u) * c2;
-      const float f4 = __uint_as_float(v.z << 16) * c2, f5 = __uint_as_float(v.z & 0xffff0000u) * c2;
-      const float f6 = __uint_as_float(v.w << 16) * c2, f7 = __uint_as_float(v.w & 0xffff0000u) * c2;
-      qf[2 * c] = (int)pack_fp8x4(sat448(f0), sat448(f1), sat448(f2), sat448(f3));
-      qf[2 * c + 1] = (int)pack_fp8x4(sat448(f4), sat448(f5), sat448(f6), sat448(f7));
+      const unsigned u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[8 * c + 2 * j] = __uint_as_float(u[j] << 16) * c2;
+        f[8 * c + 2 * j + 1] = __uint_as_float(u[j] & 0xffff0000u) * c2;
+      }
     }
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      amax = fmaxf(amax, fabsf(f[j]));
+      l1 += fabsf(f[j]);
+    }
+    l1 += __shfl_xor(l1, 32, 64);
+    const float mbound = 1.125f * l1 * kmx + 8.f;
+    const int em = f8_block_exp(mbound, -100, 100);
+    const int e1 = max(f8_block_exp(__shfl_xor(amax, 32, 64), -100, 100), em);   // hh = 1's exponent
+    const int eq = hh ? max(f8_block_exp(amax, -100, 100), em) : f8_block_exp(amax, -100, 100);
+    const int e1b = hh ? eq : e1;
+    m_up[s] = ldexpf(1.f, e1b);
+    m_dn[s] = ldexpf(1.f, -e1b);
+    qsc[s] = eq + 127;
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+      qf[s][c] = (int)pack_fp8x4(sat448(ldexpf(f[4 * c], -eq)), sat448(ldexpf(f[4 * c + 1], -eq)),
+                                 sat448(ldexpf(f[4 * c + 2], -eq)), sat448(ldexpf(f[4 * c + 3], -eq)));
   }
-  f32x16_t oacc[2];
+  f32x16_t oacc[QS][2];
 #pragma unroll
-  for (int db = 0; db < 2; ++db)
+  for (int s = 0; s < QS; ++s)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) oacc[db][r] = 0.f;
-  float mq = 0.f;
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) oacc[s][db][r] = 0.f;
+  float mq[QS];
+#pragma unroll
+  for (int s = 0; s < QS; ++s) mq[s] = 0.f;
 
-  auto compute = [&](int buf, int kv0, bool masked, bool first) {
+  auto tile_max = [&](const f32x16_t (&sa)[2]) {
+    float t[11];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const int a = 3 * k;
+      t[k] = vmax3(a < 16 ? sa[0][a] : sa[1][a - 16], a + 1 < 16 ? sa[0][a + 1] : sa[1][a + 1 - 16],
+                   a + 2 < 16 ? sa[0][a + 2] : sa[1][a + 2 - 16]);
+    }
+    t[10] = __builtin_elementwise_maximum(sa[1][14], sa[1][15]);
+    const float u0 = vmax3(t[0], t[1], t[2]), u1 = vmax3(t[3], t[4], t[5]), u2 = vmax3(t[6], t[7], t[8]);
+    const float mx = vmax3(vmax3(u0, u1, u2), t[9], t[10]);
+    unsigned w = __float_as_uint(mx);
+    const auto sw = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+    return vmax3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), mx);
+  };
+
+  auto compute = [&](int buf, int kv0, bool masked, bool first, unsigned scw) {
     const uint8_t* Ks = lds + buf * 2 * F8_IMG;
     const uint8_t* Vs = Ks + F8_IMG;
-    f32x16_t sacc[2];
+    f32x16_t sacc[QS][2];
 #pragma unroll
     for (int blk = 0; blk < 2; ++blk) {
+      const i32x8_t ka = f8_row32(Ks, 32 * blk + r32, hh);    // one K read for every subtile
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sacc[blk][r] = 0.f;
-      sacc[blk] = mma_f8(f8_row32(Ks, 32 * blk + r32, hh), qf, sacc[blk], e8_one);
+      for (int s = 0; s < QS; ++s) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[s][blk][r] = 0.f;
+        sacc[s][blk] = mma_f8(ka, qf[s], sacc[s][blk], (scw >> (8 * blk)) & 0xff, qsc[s]);
+      }
     }
     if (masked) {
 #pragma unroll
-      for (int blk = 0; blk < 2; ++blk)
+      for (int s = 0; s < QS; ++s)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (kv0 + 32 * blk + 8 * (r >> 2) + 4 * hh + (r & 3) >= p.nkv) sacc[blk][r] = -INFINITY;
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * blk + 8 * (r >> 2) + 4 * hh + (r & 3) >= p.nkv) sacc[s][blk][r] = -INFINITY;
     }
-    float mx;
-    {
-      float t[11];
+    float mx[QS];
+    bool resc = first;
 #pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        const int a = 3 * k;
-        t[k] = vmax3(a < 16 ? sacc[0][a] : sacc[1][a - 16], a + 1 < 16 ? sacc[0][a + 1] : sacc[1][a + 1 - 16],
-                     a + 2 < 16 ? sacc[0][a + 2] : sacc[1][a + 2 - 16]);
-      }
-      t[10] = __builtin_elementwise_maximum(sacc[1][14], sacc[1][15]);
-      const float u0 = vmax3(t[0], t[1], t[2]), u1 = vmax3(t[3], t[4], t[5]), u2 = vmax3(t[6], t[7], t[8]);
-      mx = vmax3(vmax3(u0, u1, u2), t[9], t[10]);
-      unsigned w = __float_as_uint(mx);
-      const auto sw = __builtin_amdgcn_permlane32_swap(w, w, false, false);
-      mx = vmax3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), mx);
+    for (int s = 0; s < QS; ++s) {
+      mx[s] = tile_max(sacc[s]);
+      resc = resc || mx[s] > kF8Top;
     }
     // accumulators are s c - ms, ms e4m3-exact (the value Q[:, 40] multiplies), held ~6 below the
     // running max: P' = 2^acc = 2^6 P lands the bulk of a flat softmax's probabilities (2^-9 .. 1)
     // in e4m3's normal range (2^-3 .. 2^6) instead of its 2^-9-step subnormals (rel-L2 at N=2048:
     // 9.2e-2 unshifted); the shift cancels in O / l (the ones row sums the same P').  Rescale when
-    // a score would pass 2^8 (P' <= 256 < 448, e4m3's max).
-    if (first || __any(mx > kF8Top)) {
-      const float want = mq + mx - kF8Shift;
-      const float tgt = first ? want : fmaxf(mq, want);
-      const int mbyte = __builtin_amdgcn_cvt_pk_fp8_f32(sat448(-tgt), 0.f, 0, false) & 0xff;
-      const float mn = -fp8_to_f(mbyte);
-      const float delta = mn - mq;
-      const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);
-      mq = mn;
-      oacc[0] *= alpha;
-      oacc[1] *= alpha;
-      sacc[0] -= delta;
-      sacc[1] -= delta;
-      if (hh == 1) qf[2] = (qf[2] & ~0xff) | mbyte;
+    // a score would pass 2^8 (P' <= 256 < 448, e4m3's max); one wave-uniform branch for all
+    // subtiles (a subtile rescaled without need only moves m up toward its max)
+    if (first || __any(resc)) {
+#pragma unroll
+      for (int s = 0; s < QS; ++s) {
+        const float want = mq[s] + mx[s] - kF8Shift;
+        const float tgt = first ? want : fmaxf(mq[s], want);
+        const int mbyte = __builtin_amdgcn_cvt_pk_fp8_f32(sat448(-tgt * m_dn[s]), 0.f, 0, false) & 0xff;
+        const float mn = -fp8_to_f(mbyte) * m_up[s];
+        const float delta = mn - mq[s];
+        const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);
+        mq[s] = mn;
+        oacc[s][0] *= alpha;
+        oacc[s][1] *= alpha;
+        sacc[s][0] -= delta;
+        sacc[s][1] -= delta;
+        if (hh == 1) qf[s][2] = (qf[s][2] & ~0xff) | mbyte;
+      }
     }
     // P^T -> e4m3 B operand: byte j = 16 blk + r
-    i32x8_t pb;
+    i32x8_t pb[QS];
 #pragma unroll
-    for (int w = 0; w < 8; ++w) {
-      const int blk = w >> 2, r0 = 4 * (w & 3);
-      pb[w] = (int)pack_fp8x4(__builtin_amdgcn_exp2f(sacc[blk][r0]), __builtin_amdgcn_exp2f(sacc[blk][r0 + 1]),
-                              __builtin_amdgcn_exp2f(sacc[blk][r0 + 2]), __builtin_amdgcn_exp2f(sacc[blk][r0 + 3]));
+    for (int s = 0; s < QS; ++s)
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        const int blk = w >> 2, r0 = 4 * (w & 3);
+        pb[s][w] = (int)pack_fp8x4(__builtin_amdgcn_exp2f(sacc[s][blk][r0]), __builtin_amdgcn_exp2f(sacc[s][blk][r0 + 1]),
+                                   __builtin_amdgcn_exp2f(sacc[s][blk][r0 + 2]), __builtin_amdgcn_exp2f(sacc[s][blk][r0 + 3]));
+      }
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const i32x8_t va = f8_row32(Vs, 32 * db + r32, hh);     // one V read for every subtile
+      const int vsc = (scw >> (16 + 8 * db)) & 0xff;
+#pragma unroll
+      for (int s = 0; s < QS; ++s) oacc[s][db] = mma_f8(va, pb[s], oacc[s][db], vsc, e8_one);
     }
-#pragma unroll
-    for (int db = 0; db < 2; ++db) oacc[db] = mma_f8(f8_row32(Vs, 32 * db + r32, hh), pb, oacc[db], e8_one);
   };
 
   const int nfull = p.nkv / 64;
+  unsigned scn = scl[0];
   issue_tile(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
-    if (t + 1 < ntiles) issue_tile(t + 1, (t + 1) & 1);
-    compute(t & 1, t * 64, t >= nfull, t == 0);
+    const unsigned scw = scn;
+    if (t + 1 < ntiles) {
+      scn = scl[(int64_t)(t + 1) * 64];
+      issue_tile(t + 1, (t + 1) & 1);
+    }
+    compute(t & 1, t * 64, t >= nfull, t == 0, scw);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
   // denominator: O^T row d = 40 = block 1 register 4 of the hh = 0 lane of this column
-  const float lt = __shfl(oacc[1][4], r32, 64);
-  const float inv = 1.0f / lt;
-  const int qi = qbase + r32;
-  if (qi < p.nq) {
-    bf16_t* orow = reinterpret_cast<bf16_t*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * HD + (int64_t)qi * p.os;
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int d = 8 * g4 + 4 * hh;
-      *reinterpret_cast<uint2*>(orow + d) =
-          make_uint2(pack_bf16x2(oacc[0][4 * g4] * inv, oacc[0][4 * g4 + 1] * inv),
-                     pack_bf16x2(oacc[0][4 * g4 + 2] * inv, oacc[0][4 * g4 + 3] * inv));
+  for (int s = 0; s < QS; ++s) {
+    const float lt = __shfl(oacc[s][1][4], r32, 64);
+    const float inv = 1.0f / lt;
+    const int qi = qbase + 32 * s + r32;
+    if (qi < p.nq) {
+      bf16_t* orow = reinterpret_cast<bf16_t*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * HD + (int64_t)qi * p.os;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 8 * g4 + 4 * hh;
+        *reinterpret_cast<uint2*>(orow + d) =
+            make_uint2(pack_bf16x2(oacc[s][0][4 * g4] * inv, oacc[s][0][4 * g4 + 1] * inv),
+                       pack_bf16x2(oacc[s][0][4 * g4 + 2] * inv, oacc[s][0][4 * g4 + 3] * inv));
+      }
+      *reinterpret_cast<uint2*>(orow + 32 + 4 * hh) =
+          make_uint2(pack_bf16x2(oacc[s][1][0] * inv, oacc[s][1][1] * inv), pack_bf16x2(oacc[s][1][2] * inv, oacc[s][1][3] * inv));
     }
-    *reinterpret_cast<uint2*>(orow + 32 + 4 * hh) =
-        make_uint2(pack_bf16x2(oacc[1][0] * inv, oacc[1][1] * inv), pack_bf16x2(oacc[1][2] * inv, oacc[1][3] * inv));
   }
 }
 
+// workspace: K8 images | V8T images | scale bytes (256 per tile) | kmax [batch][heads]
 size_t f8_workspace(const AttnArgs& a, int batch) {
-  return (size_t)2 * batch * a.heads * ((a.nkv + 63) / 64) * F8_IMG;
+  const size_t tiles = (size_t)batch * a.heads * ((a.nkv + 63) / 64);
+  return tiles * (2 * F8_IMG + 256) + (((size_t)batch * a.heads * 4 + 15) & ~(size_t)15);
 }
 
 int launch_f8_d40(const AttnArgs& a, int batch, void* ws, hipStream_t s) {
   const int ntile = (a.nkv + 63) / 64;
   uint8_t* k8 = static_cast<uint8_t*>(ws);
-  uint8_t* v8t = k8 + (size_t)batch * a.heads * ntile * F8_IMG;
-  hipLaunchKernelGGL(attn_f8_prep, dim3(ntile, a.heads, batch), dim3(256), 0, s, a, k8, v8t);
+  const size_t tiles = (size_t)batch * a.heads * ntile;
+  uint8_t* v8t = k8 + tiles * F8_IMG;
+  uint8_t* sc = v8t + tiles * F8_IMG;
+  unsigned* kmax = reinterpret_cast<unsigned*>(sc + tiles * 256);
+  if (hipMemsetAsync(kmax, 0, (size_t)batch * a.heads * 4, s) != hipSuccess) return LDM_ERR_LAUNCH;
+  hipLaunchKernelGGL(attn_f8_prep, dim3(ntile, a.heads, batch), dim3(256), 0, s, a, k8, v8t, sc, kmax);
   LDM_CHECK_LAUNCH();
-  const int e8_one = 127 + (a.heads < 0);     // E8M0 2^0 (a run-time value: see the scale notes)
+  const unsigned* scu = reinterpret_cast<const unsigned*>(sc);
+  const float* kmf = reinterpret_cast<const float*>(kmax);
+  const int e8_one = 127 + (a.heads < 0);     // E8M0 2^0 for P (kept a run-time register value)
   const int nblk = (a.nq + 255) / 256 * a.heads * batch;
-  if (nblk >= 512) hipLaunchKernelGGL((attn_f8_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a, k8, v8t, e8_one);
+  const int nb2 = (a.nq + 511) / 512 * a.heads * batch;
+  if (g_attn_qs2 && nb2 >= 256)   // 64 queries per wave (two subtiles), one 8-wave block per CU
+    hipLaunchKernelGGL((attn_f8_kernel<8, 1, 2>), dim3(nb2), dim3(512), 0, s, a, k8, v8t, scu, kmf, e8_one);
+  else if (nblk >= 512) hipLaunchKernelGGL((attn_f8_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a, k8, v8t, scu, kmf, e8_one);
   else {
     const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
-    hipLaunchKernelGGL((attn_f8_kernel<4, 2>), dim3(nb4), dim3(256), 0, s, a, k8, v8t, e8_one);
+    hipLaunchKernelGGL((attn_f8_kernel<4, 2>), dim3(nb4), dim3(256), 0, s, a, k8, v8t, scu, kmf, e8_one);
   }
   LDM_CHECK_LAUNCH();
   return LDM_OK;
@@ -2048,6 +2211,7 @@ extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 
 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
 extern "C" void ldm_attention_set_d80(int enabled) { g_attn_d80 = enabled ? 1 : 0; }
+extern "C" void ldm_attention_set_qs2(int enabled) { g_attn_qs2 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_bwd32(int enabled) { g_attn_bwd32 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_maxcol(int mode) {
   g_attn_maxcol = mode >= 1 ? 1 : 0;     // 0: per-score FMA, 16x16x32 kernel

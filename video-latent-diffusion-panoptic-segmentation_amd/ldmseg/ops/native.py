@@ -99,6 +99,7 @@ EXPORTS = {
     "ldm_attention_fwd_lse": (_i, [ctypes.POINTER(AttnParams), _vp, _vp]),
     "ldm_attention_force_legacy": (None, [_i]),
     "ldm_attention_set_d80": (None, [_i]),
+    "ldm_attention_set_qs2": (None, [_i]),
     "ldm_attention_set_bwd32": (None, [_i]),
     "ldm_conv2d_wgrad_set_ring": (None, [_i]),
     "ldm_attention_set_waves": (None, [_i]),
@@ -618,6 +619,12 @@ def set_attention_bwd32(enabled=True):
 def set_attention_d80(enabled=True):
     """Tuning / A-B hook: head_dim 80 on the 32x32x16 kernel (default) or the 16x16x32 one."""
     load_library().ldm_attention_set_d80(int(bool(enabled)))
+
+
+def set_attention_qs2(enabled=True):
+    """Tuning / A-B hook: head_dim 40 as 64 queries per wave (two subtiles sharing each K / V
+    fragment read, one 8-wave block per CU) instead of 32 (two blocks per CU)."""
+    load_library().ldm_attention_set_qs2(int(bool(enabled)))
 
 
 def force_attention_legacy(legacy=True):
