@@ -1046,23 +1046,25 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
 // fp8 attention at head_dim 40 (BASELINE config 5's 32x64 level, N = 2048) on the block-scaled
 // v_mfma_scale_f32_32x32x64_f8f6f4 with e4m3 operands: twice the bf16 MFMA rate per clock, and a
 // 64-deep K per instruction, so per 64-key tile and wave
-//   S^T = K Q^T      2 MFMAs (one per 32-key block; d = 40 + the max column padded to 64)
-//   O^T += V^T P^T   2 MFMAs (one per 32-row head-dim block, all 64 keys at once)
+//   S^T = K Q^T + (-m)  2 MFMAs (one per 32-key block; d = 40 padded to 64; the running max
+//                       enters as the C input, a splat of -m per query column)
+//   O^T += V^T P^T      2 MFMAs (one per 32-row head-dim block, all 64 keys at once)
 // against 6 + 8 x 32x32x16 bf16 issues (attn_d40_kernel).  Every 32-element operand block carries
-// its own E8M0 scale (the instruction's per-lane scale operands, free): K per (key, d half), V^T
-// per (d, key half), Q per (query, d half), chosen so the block's max lands in [224, 448] — no
-// clipping of large activations and no subnormal collapse of small ones (f8_block_exp).  P keeps
-// the unit scale (P' <= 2^8 under the lazy rescale).
+// its own E8M0 scale (the instruction's per-lane scale operands, free): K per (key, d 0..31 /
+// 32..63), V^T per (d, keys 0..31 / 32..63), Q per (query, d half), chosen so the block's max lands
+// in [224, 448] — no clipping of large activations and no subnormal collapse of small ones
+// (f8_block_exp).  A scale block is bytes 16b .. 16b + 15 of both lane halves, its scale in lane
+// half b (tools/mfma_f8_scale_probe.hip), so K and Q give lane half hh d 16hh.. and 32 + 16hh..
+// P keeps the unit scale (P' <= 2^8 under the lazy rescale).
 // K and V are quantized once per call by attn_f8_prep into 4-KB LDS images per 64-key tile (K8:
-// [key][64 B] with d = 40 set to 1.0; V8T: [d][64 keys in the P.V k order] with row 40 = 1.0,
-// the softmax denominator), 16-byte chunks XOR-swizzled so every ds_read_b128 is conflict-free;
-// the attention kernel DMAs them as they are (8 KB per tile, half the bf16 bytes).  Q is quantized
-// in registers (prescaled by scale * log2(e)) with Q[:, 40] = -m, m kept e4m3-exact, so the
-// accumulator is s c - m (the MC trick of attn_d40_kernel).
+// [key][64 B]; V8T: [d][64 keys in the P.V k order] with row 40 = 1.0, the softmax denominator)
+// plus 256 scale bytes, 16-byte chunks XOR-swizzled so every ds_read_b128 is conflict-free; the
+// attention kernel DMAs the images as they are (8 KB per tile, half the bf16 bytes).  Q is
+// quantized in registers (prescaled by scale * log2(e)).
 // ======================================================================================
 constexpr int F8_IMG = 64 * 64;              // bytes per K8 / V8T tile image
 constexpr float kF8Shift = 6.f;              // log2 of the P scale-up (see attn_f8_kernel)
-constexpr float kF8Top = 8.f;                // rescale threshold on s c - ms: P' <= 2^8
+constexpr float kF8Top = 8.f;                // rescale threshold on s c - m: P' <= 2^8
 
 __device__ __forceinline__ int f8_swz(int row, int c) { return c ^ ((row >> 2) & 3); }
 // P.V k order (the S^T accumulator registers as the B operand): byte j of lane half kb is key
@@ -1083,13 +1085,11 @@ __device__ __forceinline__ int f8_block_exp(float amax, int lo, int hi) {
   return min(max(e, lo), hi);
 }
 
-// grid (ceil(nkv / 64), heads, batch), 256 threads: one K8 and one V8T image per 64-key tile, the
-// tile's 256 E8M0 scale bytes (sc: [lane][4], byte i of lane (hh, r32) = K rows 32 i + r32 for
-// i < 2, V^T rows 32 (i - 2) + r32 for i >= 2, each over that lane's 32-element k half hh), and
-// max |K| of the (batch, head) into kmax (atomic; zeroed by the launcher)
+// grid (ceil(nkv / 64), heads, batch), 256 threads: one K8 and one V8T image per 64-key tile and
+// the tile's 256 E8M0 scale bytes (sc: [lane][4]; byte i of lane (hh, r32) = scale block hh of
+// K row 32 i + r32 for i < 2, of V^T row 32 (i - 2) + r32 for i >= 2)
 __global__ __launch_bounds__(256) void attn_f8_prep(const AttnArgs p, uint8_t* __restrict__ k8,
-                                                    uint8_t* __restrict__ v8t, uint8_t* __restrict__ sc,
-                                                    unsigned* __restrict__ kmax) {
+                                                    uint8_t* __restrict__ v8t, uint8_t* __restrict__ sc) {
   __shared__ unsigned short vs[64][66];
   const int t = blockIdx.x, h = blockIdx.y, b = blockIdx.z, ntile = gridDim.x, tid = threadIdx.x;
   const int hd = p.d;
@@ -1107,11 +1107,13 @@ __global__ __launch_bounds__(256) void attn_f8_prep(const AttnArgs p, uint8_t* _
 #pragma unroll
     for (int j = 0; j < 8; ++j) vs[key][8 * c + j] = e[j];
   }
-  // K8: row r, chunk c = d 16c .. 16c + 15; chunks 2 hh, 2 hh + 1 (threads c, c ^ 1) form one block
+  // K8: row r, chunk c = d 16c .. 16c + 15; the kernel gives lane half hh chunks hh and 2 + hh, so
+  // the instruction's scale block b (bytes 16b .. of both halves) is d 32b .. 32b + 31 = chunks 2b,
+  // 2b + 1 (threads c, c ^ 1), its scale in lane half b
   {
     const int r = tid >> 2, c = tid & 3, k = t * 64 + r;
     float f[16];
-    float amax = 0.f, kabs = 0.f;
+    float amax = 0.f;
 #pragma unroll
     for (int hv = 0; hv < 2; ++hv) {
       const int d0 = 16 * c + 8 * hv;
@@ -1119,29 +1121,24 @@ __global__ __launch_bounds__(256) void attn_f8_prep(const AttnArgs p, uint8_t* _
       if (k < p.nkv && d0 < hd) v = *reinterpret_cast<const uint4*>(kp + (int64_t)k * p.ks + d0);
       const unsigned short* e = reinterpret_cast<const unsigned short*>(&v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float x = bf16_bits_f(e[j]);
-        kabs = fmaxf(kabs, fabsf(x));
-        f[8 * hv + j] = (d0 + j == hd && k < p.nkv) ? 1.f : x;
-      }
+      for (int j = 0; j < 8; ++j) f[8 * hv + j] = bf16_bits_f(e[j]);
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) amax = fmaxf(amax, fabsf(f[j]));
     amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
-    // the max-column block (d 32 .. 63 holds d = 40 = 1.0) keeps 2^-e inside e4m3: e in [-8, 9]
-    const int e = c >= 2 ? f8_block_exp(amax, -8, 9) : f8_block_exp(amax, -100, 100);
+    const int e = f8_block_exp(amax, -100, 100);
 #pragma unroll
     for (int j = 0; j < 16; ++j) f[j] = sat448(ldexpf(f[j], -e));
     const uint4 w = make_uint4(pack_fp8x4(f[0], f[1], f[2], f[3]), pack_fp8x4(f[4], f[5], f[6], f[7]),
                                pack_fp8x4(f[8], f[9], f[10], f[11]), pack_fp8x4(f[12], f[13], f[14], f[15]));
     *reinterpret_cast<uint4*>(k8 + img + r * 64 + f8_swz(r, c) * 16) = w;
     if ((c & 1) == 0) scale[((c >> 1) * 32 + (r & 31)) * 4 + (r >> 5)] = (uint8_t)(e + 127);
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) kabs = fmaxf(kabs, __shfl_xor(kabs, o, 64));
-    if ((tid & 63) == 0) atomicMax(kmax + (int64_t)b * p.heads + h, __float_as_uint(kabs));
   }
   __syncthreads();
-  // V8T: row dr (head-dim index), chunk c = k-order positions 16c .. 16c + 15 (lane half kb = c >> 1)
+  // V8T: row dr (head-dim index), chunk c = k-order positions 16c .. 16c + 15 (lane half kb = c >> 1,
+  // bytes 16 (c & 1) ..).  The instruction's scale block b is bytes 16b .. 16b + 15 of BOTH lane
+  // halves (tools/mfma_f8_scale_probe.hip) = keys 32b .. 32b + 31: threads c, c ^ 2 form a block,
+  // its scale in lane half b = c & 1
   {
     const int dr = tid >> 2, c = tid & 3, kb = c >> 1;
     float f[16];
@@ -1155,22 +1152,26 @@ __global__ __launch_bounds__(256) void attn_f8_prep(const AttnArgs p, uint8_t* _
       f[j] = x;
       amax = fmaxf(amax, fabsf(x));
     }
-    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));
+    amax = fmaxf(amax, __shfl_xor(amax, 2, 64));
     const int e = f8_block_exp(amax, -100, 100);   // the ones row: e = -8, 2^8 exact
 #pragma unroll
     for (int j = 0; j < 16; ++j) f[j] = sat448(ldexpf(f[j], -e));
     const uint4 w = make_uint4(pack_fp8x4(f[0], f[1], f[2], f[3]), pack_fp8x4(f[4], f[5], f[6], f[7]),
                                pack_fp8x4(f[8], f[9], f[10], f[11]), pack_fp8x4(f[12], f[13], f[14], f[15]));
     *reinterpret_cast<uint4*>(v8t + img + dr * 64 + f8_swz(dr, c) * 16) = w;
-    if ((c & 1) == 0) scale[(kb * 32 + (dr & 31)) * 4 + 2 + (dr >> 5)] = (uint8_t)(e + 127);
+    if (kb == 0) scale[((c & 1) * 32 + (dr & 31)) * 4 + 2 + (dr >> 5)] = (uint8_t)(e + 127);
   }
 }
 
 typedef __attribute__((ext_vector_type(8))) int i32x8_t;
 
-// the lane's E8M0 scale bytes: sa for its A row block, sb for its B column block
+// E8M0 scales: byte OA of sa for the lane's A row block, byte OB of sb for its B column block (the
+// instruction's op_sel).  The scale words stay live across the whole tile (the tile's four scale
+// bytes in one dword): a scale extracted into its own register dies at the MFMA, and hipcc then
+// lets the 16-pass instruction's destination overlap it — every output NaN (measured)
+template <int OA, int OB>
 __device__ __forceinline__ f32x16_t mma_f8(const i32x8_t a, const i32x8_t b, f32x16_t c, int sa, int sb) {
-  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, 0, sa, 0, sb);
+  return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 0, 0, OA, sa, OB, sb);
 }
 
 // a lane's 32 bytes (chunks 2 hh, 2 hh + 1) of row `row` of a swizzled 64-byte-row image
@@ -1183,13 +1184,23 @@ __device__ __forceinline__ i32x8_t f8_row32(const uint8_t* img, int row, int hh)
   return v;
 }
 
+// the K operand: chunks hh and 2 + hh of row `row` (d 16 hh .. +16 and 32 + 16 hh .. +16), so scale
+// block b (bytes 16b .. 16b + 15 of both lane halves) is d 32b .. 32b + 31
+__device__ __forceinline__ i32x8_t f8_row32k(const uint8_t* img, int row, int hh) {
+  const uint4 lo = *reinterpret_cast<const uint4*>(img + row * 64 + f8_swz(row, hh) * 16);
+  const uint4 hi = *reinterpret_cast<const uint4*>(img + row * 64 + f8_swz(row, 2 + hh) * 16);
+  i32x8_t v;
+  v[0] = (int)lo.x; v[1] = (int)lo.y; v[2] = (int)lo.z; v[3] = (int)lo.w;
+  v[4] = (int)hi.x; v[5] = (int)hi.y; v[6] = (int)hi.z; v[7] = (int)hi.w;
+  return v;
+}
+
 __device__ __forceinline__ float fp8_to_f(int byte) { return __builtin_amdgcn_cvt_f32_fp8(byte, 0); }
 
 template <int NW, int OCC, int QS = 1>
 __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p, const uint8_t* __restrict__ k8,
                                                               const uint8_t* __restrict__ v8t,
-                                                              const unsigned* __restrict__ sc,
-                                                              const float* __restrict__ kmax, int e8_one) {
+                                                              const unsigned* __restrict__ sc, int e8_one) {
   constexpr int HD = 40;                       // head_dim (the max / ones column)
   __shared__ uint4 smem[2 * 2 * F8_IMG / 16];  // [buf][K8 | V8T]
   const uint8_t* const lds = reinterpret_cast<const uint8_t*>(smem);
@@ -1222,25 +1233,22 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
     }
   };
 
-  // Q (B operand): lane holds Q[q = qbase + 32 s + r32][d = 32 hh + j] * scale * log2(e) / 2^eq as
-  // e4m3, j < 32, its E8M0 scale eq + 127 in qsc; d = 40 (hh = 1, byte 8 = dword 2 byte 0) carries
-  // -m / 2^eq1.  eq1 (the hh = 1 block) also covers every m the loop can reach: |m| <= max |s c| + 6
-  // <= |q c|_1 max |K| + 6 (+ 1/8 for the e4m3 rounding of q and k), so -m never saturates.
+  // Q (B operand, the K operand's layout): lane half hh holds Q[q = qbase + 32 s + r32] * scale *
+  // log2(e) at d 16 hh + j (bytes j < 16, scale block 0 = d 0 .. 31) and d 32 + 16 hh + j - 16
+  // (bytes 16 .. 31, block 1 = d 32 .. 63), each block / 2^e_b as e4m3; lane half b carries e_b + 127
+  // in qsc
   const float c2 = p.scale_log2;
-  const float kmx = kmax[(int64_t)b * p.heads + h];
   i32x8_t qf[QS];
   int qsc[QS];
-  float m_up[QS], m_dn[QS];                    // 2^eq1, 2^-eq1 (the max column's scale, both lane halves)
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     const int qi = qbase + 32 * s + r32;
     const bf16_t* qrow = reinterpret_cast<const bf16_t*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * HD +
                          (int64_t)qi * p.qs;
     float f[32];
-    float amax = 0.f, l1 = 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {             // 8 d-values per 16-byte chunk
-      const int d0 = 32 * hh + 8 * c;
+      const int d0 = (c < 2 ? 16 * hh : 32 + 16 * hh) + 8 * (c & 1);
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (qi < p.nq && d0 < HD) v = *reinterpret_cast<const uint4*>(qrow + d0);
       const unsigned u[4] = {v.x, v.y, v.z, v.w};
@@ -1250,24 +1258,22 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
         f[8 * c + 2 * j + 1] = __uint_as_float(u[j] & 0xffff0000u) * c2;
       }
     }
+    float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      amax = fmaxf(amax, fabsf(f[j]));
-      l1 += fabsf(f[j]);
+    for (int j = 0; j < 16; ++j) {
+      a0 = fmaxf(a0, fabsf(f[j]));
+      a1 = fmaxf(a1, fabsf(f[16 + j]));
     }
-    l1 += __shfl_xor(l1, 32, 64);
-    const float mbound = 1.125f * l1 * kmx + 8.f;
-    const int em = f8_block_exp(mbound, -100, 100);
-    const int e1 = max(f8_block_exp(__shfl_xor(amax, 32, 64), -100, 100), em);   // hh = 1's exponent
-    const int eq = hh ? max(f8_block_exp(amax, -100, 100), em) : f8_block_exp(amax, -100, 100);
-    const int e1b = hh ? eq : e1;
-    m_up[s] = ldexpf(1.f, e1b);
-    m_dn[s] = ldexpf(1.f, -e1b);
-    qsc[s] = eq + 127;
+    a0 = fmaxf(a0, __shfl_xor(a0, 32, 64));
+    a1 = fmaxf(a1, __shfl_xor(a1, 32, 64));
+    const int e0 = f8_block_exp(a0, -100, 100), e1 = f8_block_exp(a1, -100, 100);
+    qsc[s] = (hh ? e1 : e0) + 127;
 #pragma unroll
-    for (int c = 0; c < 8; ++c)
-      qf[s][c] = (int)pack_fp8x4(sat448(ldexpf(f[4 * c], -eq)), sat448(ldexpf(f[4 * c + 1], -eq)),
-                                 sat448(ldexpf(f[4 * c + 2], -eq)), sat448(ldexpf(f[4 * c + 3], -eq)));
+    for (int c = 0; c < 8; ++c) {
+      const int e = c < 4 ? e0 : e1;
+      qf[s][c] = (int)pack_fp8x4(sat448(ldexpf(f[4 * c], -e)), sat448(ldexpf(f[4 * c + 1], -e)),
+                                 sat448(ldexpf(f[4 * c + 2], -e)), sat448(ldexpf(f[4 * c + 3], -e)));
+    }
   }
   f32x16_t oacc[QS][2];
 #pragma unroll
@@ -1276,9 +1282,17 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
     for (int db = 0; db < 2; ++db)
 #pragma unroll
       for (int r = 0; r < 16; ++r) oacc[s][db][r] = 0.f;
+  // the running max enters S^T through the MFMA's C input: negm[s] = -m in every register (a
+  // 32x32 result column is one query), so the accumulators come out as s c - m at no VALU cost and
+  // the operands carry no max column (their scale blocks see only Q and K)
   float mq[QS];
+  f32x16_t negm[QS];
 #pragma unroll
-  for (int s = 0; s < QS; ++s) mq[s] = 0.f;
+  for (int s = 0; s < QS; ++s) {
+    mq[s] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) negm[s][r] = 0.f;
+  }
 
   auto tile_max = [&](const f32x16_t (&sa)[2]) {
     float t[11];
@@ -1296,19 +1310,21 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
     return vmax3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), mx);
   };
 
+#ifdef LDM_F8_DEBUG
+  float dbg[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  dbg[0] = (float)qsc[0];
+#endif
   auto compute = [&](int buf, int kv0, bool masked, bool first, unsigned scw) {
     const uint8_t* Ks = lds + buf * 2 * F8_IMG;
     const uint8_t* Vs = Ks + F8_IMG;
     f32x16_t sacc[QS][2];
 #pragma unroll
     for (int blk = 0; blk < 2; ++blk) {
-      const i32x8_t ka = f8_row32(Ks, 32 * blk + r32, hh);    // one K read for every subtile
+      const i32x8_t ka = f8_row32k(Ks, 32 * blk + r32, hh);   // one K read for every subtile
 #pragma unroll
-      for (int s = 0; s < QS; ++s) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[s][blk][r] = 0.f;
-        sacc[s][blk] = mma_f8(ka, qf[s], sacc[s][blk], (scw >> (8 * blk)) & 0xff, qsc[s]);
-      }
+      for (int s = 0; s < QS; ++s)
+        sacc[s][blk] = blk == 0 ? mma_f8<0, 0>(ka, qf[s], negm[s], (int)scw, qsc[s])
+                                : mma_f8<1, 0>(ka, qf[s], negm[s], (int)scw, qsc[s]);
     }
     if (masked) {
 #pragma unroll
@@ -1326,8 +1342,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
       mx[s] = tile_max(sacc[s]);
       resc = resc || mx[s] > kF8Top;
     }
-    // accumulators are s c - ms, ms e4m3-exact (the value Q[:, 40] multiplies), held ~6 below the
-    // running max: P' = 2^acc = 2^6 P lands the bulk of a flat softmax's probabilities (2^-9 .. 1)
+#ifdef LDM_F8_DEBUG
+    if (first) { dbg[2] = sacc[0][0][0]; dbg[3] = mx[0]; dbg[7] = (float)scw; }
+#endif
+    // accumulators are s c - m, m held ~6 below the running max: P' = 2^acc = 2^6 P lands the bulk of a flat softmax's probabilities (2^-9 .. 1)
     // in e4m3's normal range (2^-3 .. 2^6) instead of its 2^-9-step subnormals (rel-L2 at N=2048:
     // 9.2e-2 unshifted); the shift cancels in O / l (the ones row sums the same P').  Rescale when
     // a score would pass 2^8 (P' <= 256 < 448, e4m3's max); one wave-uniform branch for all
@@ -1336,9 +1354,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
 #pragma unroll
       for (int s = 0; s < QS; ++s) {
         const float want = mq[s] + mx[s] - kF8Shift;
-        const float tgt = first ? want : fmaxf(mq[s], want);
-        const int mbyte = __builtin_amdgcn_cvt_pk_fp8_f32(sat448(-tgt * m_dn[s]), 0.f, 0, false) & 0xff;
-        const float mn = -fp8_to_f(mbyte) * m_up[s];
+        const float mn = first ? want : fmaxf(mq[s], want);
         const float delta = mn - mq[s];
         const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);
         mq[s] = mn;
@@ -1346,7 +1362,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
         oacc[s][1] *= alpha;
         sacc[s][0] -= delta;
         sacc[s][1] -= delta;
-        if (hh == 1) qf[s][2] = (qf[s][2] & ~0xff) | mbyte;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) negm[s][r] = -mn;
       }
     }
     // P^T -> e4m3 B operand: byte j = 16 blk + r
@@ -1359,12 +1376,16 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
         pb[s][w] = (int)pack_fp8x4(__builtin_amdgcn_exp2f(sacc[s][blk][r0]), __builtin_amdgcn_exp2f(sacc[s][blk][r0 + 1]),
                                    __builtin_amdgcn_exp2f(sacc[s][blk][r0 + 2]), __builtin_amdgcn_exp2f(sacc[s][blk][r0 + 3]));
       }
+#ifdef LDM_F8_DEBUG
+    if (first) { dbg[4] = mq[0]; dbg[5] = __uint_as_float((unsigned)pb[0][0]); }
+#endif
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
       const i32x8_t va = f8_row32(Vs, 32 * db + r32, hh);     // one V read for every subtile
-      const int vsc = (scw >> (16 + 8 * db)) & 0xff;
 #pragma unroll
-      for (int s = 0; s < QS; ++s) oacc[s][db] = mma_f8(va, pb[s], oacc[s][db], vsc, e8_one);
+      for (int s = 0; s < QS; ++s)
+        oacc[s][db] = db == 0 ? mma_f8<2, 0>(va, pb[s], oacc[s][db], (int)scw, e8_one)
+                              : mma_f8<3, 0>(va, pb[s], oacc[s][db], (int)scw, e8_one);
     }
   };
 
@@ -1385,6 +1406,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
   }
 
   // denominator: O^T row d = 40 = block 1 register 4 of the hh = 0 lane of this column
+#ifdef LDM_F8_DEBUG
+  dbg[6] = oacc[0][1][4];
+  if (p.lse && blockIdx.x == 0)
+    for (int i = 0; i < 8; ++i) p.lse[tid * 8 + i] = dbg[i];
+#endif
 #pragma unroll
   for (int s = 0; s < QS; ++s) {
     const float lt = __shfl(oacc[s][1][4], r32, 64);
@@ -1405,33 +1431,36 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
   }
 }
 
-// workspace: K8 images | V8T images | scale bytes (256 per tile) | kmax [batch][heads]
+// workspace: K8 images | V8T images | scale bytes (256 per tile)
 size_t f8_workspace(const AttnArgs& a, int batch) {
-  const size_t tiles = (size_t)batch * a.heads * ((a.nkv + 63) / 64);
-  return tiles * (2 * F8_IMG + 256) + (((size_t)batch * a.heads * 4 + 15) & ~(size_t)15);
+  return (size_t)batch * a.heads * ((a.nkv + 63) / 64) * (2 * F8_IMG + 256);
 }
 
-int launch_f8_d40(const AttnArgs& a, int batch, void* ws, hipStream_t s) {
+#ifdef LDM_F8_DEBUG
+float* g_f8_dbg = nullptr;
+#endif
+int launch_f8_d40(const AttnArgs& a0, int batch, void* ws, hipStream_t s) {
+  AttnArgs a = a0;
+#ifdef LDM_F8_DEBUG
+  a.lse = g_f8_dbg;
+#endif
   const int ntile = (a.nkv + 63) / 64;
   uint8_t* k8 = static_cast<uint8_t*>(ws);
   const size_t tiles = (size_t)batch * a.heads * ntile;
   uint8_t* v8t = k8 + tiles * F8_IMG;
   uint8_t* sc = v8t + tiles * F8_IMG;
-  unsigned* kmax = reinterpret_cast<unsigned*>(sc + tiles * 256);
-  if (hipMemsetAsync(kmax, 0, (size_t)batch * a.heads * 4, s) != hipSuccess) return LDM_ERR_LAUNCH;
-  hipLaunchKernelGGL(attn_f8_prep, dim3(ntile, a.heads, batch), dim3(256), 0, s, a, k8, v8t, sc, kmax);
+  hipLaunchKernelGGL(attn_f8_prep, dim3(ntile, a.heads, batch), dim3(256), 0, s, a, k8, v8t, sc);
   LDM_CHECK_LAUNCH();
   const unsigned* scu = reinterpret_cast<const unsigned*>(sc);
-  const float* kmf = reinterpret_cast<const float*>(kmax);
   const int e8_one = 127 + (a.heads < 0);     // E8M0 2^0 for P (kept a run-time register value)
   const int nblk = (a.nq + 255) / 256 * a.heads * batch;
   const int nb2 = (a.nq + 511) / 512 * a.heads * batch;
   if (g_attn_qs2 && nb2 >= 256)   // 64 queries per wave (two subtiles), one 8-wave block per CU
-    hipLaunchKernelGGL((attn_f8_kernel<8, 1, 2>), dim3(nb2), dim3(512), 0, s, a, k8, v8t, scu, kmf, e8_one);
-  else if (nblk >= 512) hipLaunchKernelGGL((attn_f8_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a, k8, v8t, scu, kmf, e8_one);
+    hipLaunchKernelGGL((attn_f8_kernel<8, 1, 2>), dim3(nb2), dim3(512), 0, s, a, k8, v8t, scu, e8_one);
+  else if (nblk >= 512) hipLaunchKernelGGL((attn_f8_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a, k8, v8t, scu, e8_one);
   else {
     const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
-    hipLaunchKernelGGL((attn_f8_kernel<4, 2>), dim3(nb4), dim3(256), 0, s, a, k8, v8t, scu, kmf, e8_one);
+    hipLaunchKernelGGL((attn_f8_kernel<4, 2>), dim3(nb4), dim3(256), 0, s, a, k8, v8t, scu, e8_one);
   }
   LDM_CHECK_LAUNCH();
   return LDM_OK;
@@ -2206,6 +2235,9 @@ extern "C" int ldm_attention_fp8(const ldm_attn_params* q, void* workspace, int6
 }
 
 extern "C" void ldm_attention_set_fp8_scaled(int enabled) { g_fp8_scaled = enabled ? 1 : 0; }
+#ifdef LDM_F8_DEBUG
+extern "C" void ldm_f8_debug_buffer(float* p) { g_f8_dbg = p; }
+#endif
 
 extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 || waves == 8) ? waves : 0; }
 
