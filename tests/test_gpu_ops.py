@@ -313,12 +313,14 @@ def test_attention_d80_forms_agree(B, N):
     assert torch.allclose(outs[0][1], outs[1][1], atol=2e-2)
 
 
-@pytest.mark.parametrize("B,N", [(4, 4096), (4, 4096 + 37)])
+@pytest.mark.parametrize("B,N", [(4, 4096), (4, 4096 + 37), (4, 64 * 3 + 5)])
 def test_attention_d40_qs2_close_to_default(B, N):
-    """head_dim 40 with two 32-query subtiles per wave (ldm_attention_set_qs2) against the default
-    one-subtile kernel and a torch fp32 reference on the device: within the bf16 bar, and within
-    bf16 rounding of each other (the shared rescale decision moves m by different bf16 steps, so
-    not bit-identical); a ragged N exercises the masked last key tile and the partial query block."""
+    """head_dim 40 under the alternative kernels of ldm_attention_set_qs2 against the default and a
+    torch fp32 reference on the device: mode 1 (two 32-query subtiles per wave; the shared rescale
+    decision moves m by different bf16 steps, so within bf16 rounding, not bit-identical) and mode 2
+    (the software-pipelined tile loop: the same operations per query, bit-identical).  Ragged N
+    exercises the masked last key tile and the partial query block; N = 197 gives 4 key tiles (the
+    pipeline's two-tile unroll with an odd tail)."""
     torch.manual_seed(9)
     C, H = 320, 8
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(torch.bfloat16)
@@ -327,14 +329,15 @@ def test_attention_d40_qs2_close_to_default(B, N):
                      for b in range(B)]).permute(0, 2, 1, 3).reshape(B, N, C)
     outs = []
     try:
-        for on in (False, True):
-            K.set_attention_qs2(on)
+        for mode in (0, 1, 2):
+            K.set_attention_qs2(mode)
             outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, 40, N, N, 3 * C, 3 * C, 3 * C).float())
     finally:
-        K.set_attention_qs2(False)
+        K.set_attention_qs2(0)
     for o in outs:
         assert ((o - ref).norm() / ref.norm()).item() < 1e-2
     assert (outs[0] - outs[1]).abs().max().item() < 0.05
+    assert torch.equal(outs[0], outs[2])
 
 
 def test_attention_softmax_spike():

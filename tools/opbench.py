@@ -49,7 +49,7 @@ def mm_case(M, K, N):
     return (lambda: torch.mm(a, b)), 2.0 * M * K * N, None
 
 
-def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True, d80=True, qs2=False):
+def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True, d80=True, qs2=0):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
     def run():
@@ -250,9 +250,11 @@ CASES = {
     "attn_c5_2048_d40_fp8": lambda: attn_case(16, 2048, 320, fp8=True),
     "attn_c5_2048_d40_fp8pv": lambda: attn_case(16, 2048, 320, fp8=True, scaled=False),
     "attn_4096_d40_fp8": lambda: attn_case(8, 4096, 320, fp8=True),
-    "attn_4096_d40_qs2": lambda: attn_case(8, 4096, 320, qs2=True),
-    "attn_c5_2048_d40_qs2": lambda: attn_case(16, 2048, 320, qs2=True),
-    "attn_c5_2048_d40_fp8_qs2": lambda: attn_case(16, 2048, 320, fp8=True, qs2=True),
+    "attn_4096_d40_qs2": lambda: attn_case(8, 4096, 320, qs2=1),
+    "attn_4096_d40_pipe": lambda: attn_case(8, 4096, 320, qs2=2),
+    "attn_c5_2048_d40_qs2": lambda: attn_case(16, 2048, 320, qs2=1),
+    "attn_c5_2048_d40_pipe": lambda: attn_case(16, 2048, 320, qs2=2),
+    "attn_c5_2048_d40_fp8_qs2": lambda: attn_case(16, 2048, 320, fp8=True, qs2=1),
     "attn_4096_d40_fma": lambda: attn_case(8, 4096, 320, maxcol=0),
     "attn_4096_d40_mc16": lambda: attn_case(8, 4096, 320, maxcol=1),
     "attn_1024_d80_fma": lambda: attn_case(8, 1024, 640, maxcol=0),

@@ -951,6 +951,277 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   }
 }
 
+// buffer LDS-DMA of 16 bytes per lane (igemm_common.h's dma16s: per-lane offset in one VGPR, the
+// wave-uniform part in soffset; out-of-range offsets read zeros)
+__device__ __forceinline__ void attn_dma16s(__amdgpu_buffer_rsrc_t rsrc, int voff, int soff, unsigned lds_addr) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %4\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %3 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds_addr)
+      : "memory");
+}
+
+// head_dim 40 with the tile loop software-pipelined inside each wave: Q.K^T of tile t + 1 is issued
+// beside the softmax exp / cvt of tile t, and P.V of tile t beside the rest of it, in one
+// branch-free region whose interleave is fixed with sched_group_barrier (attn_d40_kernel's waves
+// are phase-locked by the per-tile barrier: all of a block's waves issue Q.K^T, then all run the
+// softmax VALU with the matrix pipe idle).  P.V(t) reads tile t's V while Q.K^T reads tile t + 1's
+// K and tile t + 2 streams in: three LDS buffers.  The K / V tiles arrive by buffer LDS-DMA with
+// one lane offset per slot (rows past n_kv read zeros); the max / ones columns (d = 40) are
+// written once into every buffer and never DMA'd.  Same arithmetic per query as attn_d40_kernel
+// (max column, ones column, bf16 P): bit-identical results.  8 waves x 32 queries per block.
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 1) void attn_d40p_kernel(const AttnArgs p) {
+  typedef bf16_t T;
+  typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+  constexpr int D = 40, KT = 64, QC = 3, ND32 = 2;
+  constexpr int EPC = 8, RCH = 9, ROW = RCH * EPC, TILE = KT * ROW, ES = 2, NBUF = 3;
+  constexpr int DCH = D / EPC;                     // data chunks per row (5); chunk 5 = max / ones
+  __shared__ uint4 smem[NBUF * 2 * TILE * ES / 16];
+  T* const lds = reinterpret_cast<T*>(smem);
+  typedef __attribute__((address_space(3))) uint4 lds_u4_t;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r32 = lane & 31, hh = lane >> 5, i16 = lane & 15;
+  int qb, h, b;
+  {
+    const int nqb = (p.nq + 32 * NW - 1) / (32 * NW);
+    const int bid = blockIdx.x, nblk = gridDim.x;
+    const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
+    const int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    qb = t % nqb;
+    const int hb = t / nqb;
+    h = hb % p.heads;
+    b = hb / p.heads;
+  }
+  const int qbase = qb * (32 * NW) + wave * 32;
+  const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * D;
+  const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * D;
+  const T* vp = reinterpret_cast<const T*>(p.v) + (int64_t)b * p.nkv * p.vs + (int64_t)h * D;
+  const __amdgpu_buffer_rsrc_t rk =
+      __builtin_amdgcn_make_buffer_rsrc((void*)kp, 0, (int)(((int64_t)(p.nkv - 1) * p.ks + D) * ES), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv =
+      __builtin_amdgcn_make_buffer_rsrc((void*)vp, 0, (int)(((int64_t)(p.nkv - 1) * p.vs + D) * ES), 0x00020000);
+
+  // constant columns: chunk 5 of every row = (1.0, 0 ...) in K (max column) and V (ones column),
+  // chunks 6..8 zero; the DMA below writes data chunks 0..4 only
+  for (int i = tid; i < NBUF * 2 * KT * (RCH - DCH); i += 64 * NW) {
+    const int c = DCH + i % (RCH - DCH), row = (i / (RCH - DCH)) % (NBUF * 2 * KT);
+    smem[row * RCH + c] = c == DCH ? kOnesBf16 : kZeros16;
+  }
+  // DMA slots: instruction i (of RCH per tile and operand) covers 64 consecutive 16-byte chunks of
+  // the [64 rows][9 chunks] tile; lanes of data chunks carry a fixed row offset, the rest are
+  // masked off (exec) so the constant columns stay
+  constexpr int NSL = (RCH + NW - 1) / NW;
+  int koff[NSL], voff[NSL];
+  bool dat[NSL];
+#pragma unroll
+  for (int s2 = 0; s2 < NSL; ++s2) {
+    const int i = wave + NW * s2;
+    const int L = i * 64 + lane;
+    const int row = L / RCH, c = L - row * RCH;
+    dat[s2] = i < RCH && c < DCH;
+    koff[s2] = (row * p.ks + c * EPC) * ES;
+    voff[s2] = (row * p.vs + c * EPC) * ES;
+  }
+  auto issue = [&](int t, int buf) __attribute__((always_inline)) {
+    const unsigned kb = lds0 + (unsigned)(buf * 2 * TILE * ES);
+    const unsigned vb = kb + TILE * ES;
+    const int ktile = t * KT * p.ks * ES, vtile = t * KT * p.vs * ES;
+#pragma unroll
+    for (int s2 = 0; s2 < NSL; ++s2) {
+      const int i = wave + NW * s2;
+      if (i >= RCH) break;
+      const unsigned off = __builtin_amdgcn_readfirstlane(i * 64 * 16);
+      if (dat[s2]) {
+        attn_dma16s(rk, koff[s2], __builtin_amdgcn_readfirstlane(ktile), __builtin_amdgcn_readfirstlane(kb + off));
+        attn_dma16s(rv, voff[s2], __builtin_amdgcn_readfirstlane(vtile), __builtin_amdgcn_readfirstlane(vb + off));
+      }
+    }
+  };
+  const float c2 = p.scale_log2;
+  uint4 qf[QC];
+  {
+    const int qi = qbase + r32;
+    const T* qrow = qp + (int64_t)qi * p.qs;
+#pragma unroll
+    for (int c = 0; c < QC; ++c) {
+      const int dd = 16 * c + 8 * hh;
+      if (qi < p.nq && dd < D) qf[c] = scale_bf16x8(*reinterpret_cast<const uint4*>(qrow + dd), c2);
+      else qf[c] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  f32x16_t oacc[ND32], sacc[2][2];   // sacc[c]: score slot c (tile being finished / next tile)
+  float mq = 0.f;
+#pragma unroll
+  for (int db = 0; db < ND32; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) oacc[db][r] = 0.f;
+  typedef __attribute__((ext_vector_type(4))) short s4_t;
+  typedef __attribute__((address_space(3))) s4_t lds_s4_t;
+
+  auto qk = [&](int s, int buf) __attribute__((always_inline)) {
+    const T* Ks = lds + buf * 2 * TILE;
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[s][blk][r] = 0.f;
+      const T* krow = Ks + (32 * blk + r32) * ROW + 8 * hh;
+#pragma unroll
+      for (int c = 0; c < QC; ++c) {
+        const uint4 ka = *reinterpret_cast<const uint4*>(krow + 16 * c);
+        sacc[s][blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, ka),
+                                                               __builtin_bit_cast(bf16x8_t, qf[c]), sacc[s][blk], 0, 0, 0);
+      }
+    }
+  };
+  auto mask = [&](int s, int kv0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (kv0 + 32 * blk + 8 * (r >> 2) + 4 * hh + (r & 3) >= p.nkv) sacc[s][blk][r] = -INFINITY;
+  };
+  auto smax = [&](int s) __attribute__((always_inline)) {
+    float t[11];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const int a = 3 * k;
+      t[k] = vmax3(a < 16 ? sacc[s][0][a] : sacc[s][1][a - 16], a + 1 < 16 ? sacc[s][0][a + 1] : sacc[s][1][a + 1 - 16],
+                   a + 2 < 16 ? sacc[s][0][a + 2] : sacc[s][1][a + 2 - 16]);
+    }
+    t[10] = __builtin_elementwise_maximum(sacc[s][1][14], sacc[s][1][15]);
+    const float u0 = vmax3(t[0], t[1], t[2]), u1 = vmax3(t[3], t[4], t[5]), u2 = vmax3(t[6], t[7], t[8]);
+    float mx = vmax3(vmax3(u0, u1, u2), t[9], t[10]);
+    unsigned w = __float_as_uint(mx);
+    const auto sw = __builtin_amdgcn_permlane32_swap(w, w, false, false);
+    return vmax3(__uint_as_float(sw[0]), __uint_as_float(sw[1]), mx);
+  };
+  auto rescale = [&](int s, float mx, bool first) __attribute__((always_inline)) {
+    if (first || __any(mx > kRescaleThr)) {
+      const float tgt = mq + mx;
+      const float mn = bf16_rne(first ? tgt : fmaxf(mq, tgt));
+      const float delta = mn - mq;
+      const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);
+      mq = mn;
+#pragma unroll
+      for (int db = 0; db < ND32; ++db) oacc[db] *= alpha;
+      sacc[s][0] -= delta;
+      sacc[s][1] -= delta;
+      if (hh == (D % 16) / 8) qf[D / 16].x = (qf[D / 16].x & 0xffff0000u) | (__float_as_uint(-mn) >> 16);
+    }
+  };
+  // this tile's softmax + P.V (slot s, V of buffer buf) beside the next tile's Q.K^T (slot s ^ 1)
+  auto body = [&](int s, int buf, int nbuf, bool next) __attribute__((always_inline)) {
+    if (next) qk(s ^ 1, nbuf);
+    uint4 pb[2][2];
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        float pv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pv[j] = __builtin_amdgcn_exp2f(sacc[s][blk][8 * st + j]);
+        pb[blk][st] = make_uint4(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]), pack_bf16x2(pv[4], pv[5]),
+                                 pack_bf16x2(pv[6], pv[7]));
+      }
+    const T* Vs = lds + buf * 2 * TILE + TILE;
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int db = 0; db < ND32; ++db) {
+          const int cb = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+          const T* a0 = Vs + (32 * blk + 16 * st + 4 * hh + (i16 >> 2)) * ROW + cb;
+          const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0)));
+          const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0 + 8 * ROW)));
+          const uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
+          oacc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, va),
+                                                             __builtin_bit_cast(bf16x8_t, pb[blk][st]), oacc[db], 0, 0, 0);
+        }
+    if (next) {
+      // Q.K^T(next): 6 MFMAs, each beside one K read, four exp and two other VALU; then the P.V
+      // MFMAs, each beside two V reads, one exp and two other VALU (masks: DS read 0x100, MFMA 0x8,
+      // transcendental 0x400, VALU 0x2)
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        if (k + 1 < 6) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x400, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x400, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+    }
+  };
+
+  const int ntiles = (p.nkv + KT - 1) / KT;
+  const int nfull = p.nkv / KT;
+  issue(0, 0);
+  if (1 < ntiles) issue(1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  qk(0, 0);
+  if (nfull == 0) mask(0, 0);
+  rescale(0, smax(0), true);
+  // tiles 0 .. ntiles - 2 have a next tile; the loop runs in pairs so score slots are compile-time
+  auto step = [&](int s, int t) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // tile t + 1 landed for every wave; tile t - 1's buffer is free
+    if (t + 2 < ntiles) issue(t + 2, (t + 2) % NBUF);
+    body(s, t % NBUF, (t + 1) % NBUF, true);
+    if (t + 1 >= nfull) mask(s ^ 1, (t + 1) * KT);
+    rescale(s ^ 1, smax(s ^ 1), false);
+  };
+  int t = 0;
+  for (; t + 2 < ntiles; t += 2) {
+    step(0, t);
+    step(1, t + 1);
+  }
+  if (t + 1 < ntiles) {
+    step(0, t);
+    ++t;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    body(1, t % NBUF, 0, false);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    body(0, t % NBUF, 0, false);
+  }
+
+  const float lt = __shfl(oacc[D / 32][4 * ((D % 32) / 8)], r32, 64);
+  const float inv = 1.0f / lt;
+  const int qi = qbase + r32;
+  if (qi < p.nq) {
+    if (p.lse && hh == 0) p.lse[((int64_t)b * p.heads + h) * p.nq + qi] = mq + __log2f(lt);
+    T* orow = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * D + (int64_t)qi * p.os;
+#pragma unroll
+    for (int db = 0; db < ND32; ++db)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int d = 32 * db + 8 * g4 + 4 * hh;
+        if (32 * db + 8 * g4 >= D) break;
+        *reinterpret_cast<uint2*>(orow + d) =
+            make_uint2(pack_bf16x2(oacc[db][4 * g4] * inv, oacc[db][4 * g4 + 1] * inv),
+                       pack_bf16x2(oacc[db][4 * g4 + 2] * inv, oacc[db][4 * g4 + 3] * inv));
+      }
+  }
+}
+
 int g_attn_waves = 0;   // 0: auto (8 when that still gives >= 256 blocks), 4 or 8: forced
 
 template <int DP, int QSUB, bool ONES, bool F8 = false, bool MC = false>
@@ -997,7 +1268,8 @@ int launch32_dp_mc(const AttnArgs& a, int batch, hipStream_t s) {
 }
 
 int g_attn_d80 = 1;      // tuning / A-B hook: 0 routes head_dim 80 to the 16x16x32 kernel
-int g_attn_qs2 = 0;      // tuning / A-B hook: 1 runs head_dim 40 as 64 queries per wave (two subtiles)
+int g_attn_qs2 = 0;      // tuning / A-B hook: head_dim 40 as 64 queries per wave: 1 two subtiles in step,
+                         // 2 the pipelined form (attn_d40p_kernel)
 
 template <int DP, bool F8 = false>
 int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
@@ -1021,7 +1293,10 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
       // (measured at N=4096: 8 waves x 2 blocks per CU 241 us; 4 waves x 4 blocks 302 us — each K/V
       // tile then serves half the queries; 128-key tiles 249 us)
       const int nb2 = (a.nq + 511) / 512 * a.heads * batch;
-      if (g_attn_qs2 && g_attn_waves == 0 && nb2 >= 256) {
+      if (g_attn_qs2 == 2 && g_attn_waves == 0) {
+        // 8 waves x 32 queries, the tile loop software-pipelined inside each wave
+        hipLaunchKernelGGL((attn_d40p_kernel<8>), dim3(nblk), dim3(512), 0, s, a);
+      } else if (g_attn_qs2 == 1 && g_attn_waves == 0 && nb2 >= 256) {
         // 8 waves x 64 queries (two subtiles sharing every K / V fragment read), one block per CU
         hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 40, 2>), dim3(nb2), dim3(512), 0, s, a);
       } else if (g_attn_waves == 4) {
@@ -1455,7 +1730,7 @@ int launch_f8_d40(const AttnArgs& a0, int batch, void* ws, hipStream_t s) {
   const int e8_one = 127 + (a.heads < 0);     // E8M0 2^0 for P (kept a run-time register value)
   const int nblk = (a.nq + 255) / 256 * a.heads * batch;
   const int nb2 = (a.nq + 511) / 512 * a.heads * batch;
-  if (g_attn_qs2 && nb2 >= 256)   // 64 queries per wave (two subtiles), one 8-wave block per CU
+  if (g_attn_qs2 == 1 && nb2 >= 256)   // 64 queries per wave (two subtiles), one 8-wave block per CU
     hipLaunchKernelGGL((attn_f8_kernel<8, 1, 2>), dim3(nb2), dim3(512), 0, s, a, k8, v8t, scu, e8_one);
   else if (nblk >= 512) hipLaunchKernelGGL((attn_f8_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a, k8, v8t, scu, e8_one);
   else {
@@ -2243,7 +2518,7 @@ extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 
 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
 extern "C" void ldm_attention_set_d80(int enabled) { g_attn_d80 = enabled ? 1 : 0; }
-extern "C" void ldm_attention_set_qs2(int enabled) { g_attn_qs2 = enabled ? 1 : 0; }
+extern "C" void ldm_attention_set_qs2(int mode) { g_attn_qs2 = mode == 1 || mode == 2 ? mode : 0; }
 extern "C" void ldm_attention_set_bwd32(int enabled) { g_attn_bwd32 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_maxcol(int mode) {
   g_attn_maxcol = mode >= 1 ? 1 : 0;     // 0: per-score FMA, 16x16x32 kernel

@@ -621,10 +621,11 @@ def set_attention_d80(enabled=True):
     load_library().ldm_attention_set_d80(int(bool(enabled)))
 
 
-def set_attention_qs2(enabled=True):
-    """Tuning / A-B hook: head_dim 40 as 64 queries per wave (two subtiles sharing each K / V
-    fragment read, one 8-wave block per CU) instead of 32 (two blocks per CU)."""
-    load_library().ldm_attention_set_qs2(int(bool(enabled)))
+def set_attention_qs2(mode=1):
+    """Tuning / A-B hook for head_dim 40: 0 the default kernel (32 queries per wave, two 8-wave
+    blocks per CU); 1 two 32-query subtiles per wave sharing each K / V fragment read (one block per
+    CU); 2 the tile loop software-pipelined inside each wave (attn_d40p_kernel)."""
+    load_library().ldm_attention_set_qs2(int(mode))
 
 
 def force_attention_legacy(legacy=True):
