@@ -284,6 +284,9 @@ class PackedConv:
             b = None if bias is None else bias.detach().float()
             self.ksize, self.cin, self.n = 2, cin, cout
             self.cin_real = cin
+            # the gather form for images the phase kernel cannot tile (a tile's rows must lie in one
+            # phase: h * w % 32 == 0); packed now, so a captured graph never packs
+            self.gather = PackedConv(weight, bias, dtype)
         elif convt4:
             # ConvTranspose2d(k=4, s=2, p=1) weight [cin, cout, 4, 4] as a 3x3 conv (pad 1) with
             # 4 * cout outputs, one per output phase (dy, dx), + the pixel-shuffle epilogue:
@@ -458,9 +461,13 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
         _contig(t, nm)
     if x0.dtype != pc.dtype or (x1 is not None and x1.dtype != pc.dtype):
         raise TypeError(f"conv input dtype {x0.dtype} != packed weight dtype {pc.dtype}")
+    if getattr(pc, "phases", False):
+        if not upsample:
+            raise ValueError("an upsample_phases pack is the nearest-2x upsample conv: pass upsample=True")
+        if (h * w) % 32 or x1 is not None or stride != 1 or pad_mode or out_layout != OUT_NHWC or \
+                row_stats is not None or ln is not None:
+            pc = pc.gather                 # shapes the phase form does not take: the 3x3 gather form
     k = pc.ksize
-    if getattr(pc, "phases", False) and not upsample:
-        raise ValueError("an upsample_phases pack is the nearest-2x upsample conv: pass upsample=True")
     if k == 1:
         ho, wo = h, w
     elif upsample:
