@@ -544,7 +544,8 @@ class UNet(nn.Module):
 
     @property
     def upsample_phases(self):
-        return getattr(self, "_up_phases", True)
+        # inference only: the autograd drop-in (train mode) differentiates the 3x3 gather form
+        return getattr(self, "_up_phases", True) and not self.training
 
     def set_upsample_phases(self, enabled=True):
         """Run every Upsample2D conv as four 2x2 phase convs over its low-res input (default on:

@@ -90,7 +90,7 @@ class LDMTrainStep:
         # plain layout of its parameters, refreshed in place after each update (models/repack.py).
         # The module's inference setting is restored inside ``for_inference()`` (validation sampling)
         self._inference_fold = unet.ln_fold
-        self._inference_phases = unet.upsample_phases
+        self._inference_phases = getattr(unet, "_up_phases", True)   # the setting, not its train-mode value
         unet.set_ln_fold(False)
         unet.set_upsample_phases(False)           # the backward differentiates the 3x3 upsample conv
         self.refresher = PackRefresher(unet)
