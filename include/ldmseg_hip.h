@@ -132,6 +132,9 @@ void ldm_conv2d_set_raster_group(int group_m);
 void ldm_conv2d_set_halo(int mode);
 /* Tuning hook: force the split-K factor of the 16x16 whole-image halo tiles (0 = planner). */
 void ldm_conv2d_set_halo_split(int ksplit);
+/* tuning hook: output rows per halo tile at the 32x32 level: 0 planner (8 for >= 1280 input channels,
+ * else 4), 4 or 8 forced (8: 256-row tiles, K split over channel blocks as at the 16x16 level) */
+void ldm_conv2d_set_halo_rows32(int rows);
 /* Tuning hook: the A-register-stationary bf16 1x1 GEMM (K = 320, N a multiple of 160, NHWC or
  * GEGLU, no time embedding / GroupNorm partials): 0 = planner's choice (the 64x64 UNet level),
  * 1 = never, 2 = whenever legal. */

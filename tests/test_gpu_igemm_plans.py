@@ -157,6 +157,10 @@ HALO_SHAPES = [
     ("w32_640", 2, 640, 0, 8, 32, 640),
     ("w32_concat_1280_640", 1, 1280, 640, 4, 32, 640),
     ("w32_64ch", 1, 64, 0, 12, 32, 160),
+    # 256-row tiles at width 32 (8 rows), K split over channel blocks (the wide up-block concats)
+    ("w32_r8_concat_1280_640_split2", 1, 1280, 640, 8, 32, 640),
+    ("w32_r8_concat_640_640_split3", 2, 640, 640, 16, 32, 320),
+    ("w32_r8_640_one_split", 1, 640, 0, 16, 32, 160),
     # whole 16x16 images, K split over channel blocks (fp32 slab + reduction)
     ("w16_1280_split4", 2, 1280, 0, 16, 16, 320),
     ("w16_concat_640_640_split3", 1, 640, 640, 16, 16, 320),
@@ -170,6 +174,7 @@ def halo_on():
     yield
     K.set_conv_halo(0)
     K.set_conv_halo_split(0)
+    K.set_conv_halo_rows32(0)
 
 
 @pytest.mark.parametrize("case", HALO_SHAPES, ids=[c[0] for c in HALO_SHAPES])
@@ -179,7 +184,9 @@ def test_halo_conv(case, epi, halo_on):
     LDS) vs torch fp32: time embedding + SiLU + residual epilogue, plain, and the GroupNorm
     partials through a following GroupNorm.  Bar 2e-2 (bf16 storage) / 3e-2 after GroupNorm."""
     name, B, c0, c1, H, W, Co = case
-    if W == 16:
+    if W == 32:
+        K.set_conv_halo_rows32(8 if "_r8" in name else 4)
+    if W == 16 or "_r8" in name:
         K.set_conv_halo_split(int(name.split("split")[-1]) if name[-1].isdigit() else 1)
     torch.manual_seed(11)
     x = torch.randn(B, c0 + c1, H, W)

@@ -34,6 +34,13 @@ def test_headline_plans_pinned():
         pl = _p(batch=8, h=16, w=16, c0=c0, c1=c1, n=1280, temb=True, gn_stats=True)
         assert (pl["kind"], pl["bm"], pl["bn"], pl["ksplit"]) == ("halo", 256, 160, ks), pl
         assert pl["blocks"] >= 256 and (c0 + c1) // 64 // ks >= 4, pl
+    # the 32x32 level's wide up-block concats: 256-row halo tiles split over channel blocks (the
+    # [640 || 320] -> 640 concat and the single-source convs keep 4-row tiles)
+    for c0, c1, ks in ((1280, 640, 2), (640, 640, 2)):
+        pl = _p(batch=8, h=32, w=32, c0=c0, c1=c1, n=640, temb=True, gn_stats=True)
+        assert (pl["kind"], pl["bm"], pl["bn"], pl["ksplit"], pl["blocks"]) == ("halo", 256, 160, ks, 256), pl
+    pl = _p(batch=8, h=32, w=32, c0=640, c1=320, n=640, temb=True, gn_stats=True)
+    assert (pl["kind"], pl["bm"], pl["ksplit"]) == ("halo", 128, 1), pl
     # 640 -> 1280 would need 2-channel-block splits: the split 128x160 tiles stay faster
     pl = _p(batch=8, h=16, w=16, c0=640, n=1280, temb=True, gn_stats=True)
     assert (pl["kind"], pl["bm"], pl["bn"], pl["ksplit"]) == ("tile", 128, 160, 4), pl

@@ -23,7 +23,7 @@ BATCH = 8          # --batch: the conv / GEMM cases' B (their shapes are written
 
 
 def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, geglu=False, residual=False,
-              temb=False, stats=False, c1=0, phases=False):
+              temb=False, stats=False, c1=0, phases=False, rows32=0):
     B = max(1, B * BATCH // 8)
     g = torch.Generator(device=DEV).manual_seed(0)
     x0 = torch.randn(B, H, W, Cin - c1, device=DEV, generator=g).to(BF)
@@ -36,6 +36,7 @@ def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, ge
     out_layout = K.OUT_GEGLU if geglu else layout
 
     def run():
+        K.set_conv_halo_rows32(rows32)
         return K.conv2d(pc, x0, B, H, W, x1=x1, stride=stride, upsample=up, residual=res, temb=te,
                         temb_stride=Cout if temb else 0, out_layout=out_layout, gn_stats=stats)
     flops = 2.0 * B * ho * wo * Cout * (4 if phases else k * k) * Cin     # executed (phase form: 4 taps)
@@ -199,6 +200,13 @@ CASES = {
     "gemm_ff2_2560": lambda: conv_case(8, 32, 32, 2560, 640, k=1, residual=True),
     "gemm_proj_640": lambda: conv_case(8, 32, 32, 640, 640, k=1, residual=True),
     "conv3_up_l1_1920": lambda: conv_case(8, 32, 32, 1920, 640, c1=640, residual=True, stats=True),
+    "conv3_up_l1_1920_r8": lambda: conv_case(8, 32, 32, 1920, 640, c1=640, residual=True, stats=True, rows32=8),
+    "conv3_up_l1_1280": lambda: conv_case(8, 32, 32, 1280, 640, c1=640, temb=True, stats=True),
+    "conv3_up_l1_1280_r8": lambda: conv_case(8, 32, 32, 1280, 640, c1=640, temb=True, stats=True, rows32=8),
+    "conv3_up_l1_960": lambda: conv_case(8, 32, 32, 960, 640, c1=320, temb=True, stats=True),
+    "conv3_up_l1_960_r8": lambda: conv_case(8, 32, 32, 960, 640, c1=320, temb=True, stats=True, rows32=8),
+    "conv3_l1_640_r8": lambda: conv_case(8, 32, 32, 640, 640, temb=True, stats=True, rows32=8),
+    "conv3_l1_in_320_r8": lambda: conv_case(8, 32, 32, 320, 640, temb=True, stats=True, rows32=8),
     "conv3_upsample_320": lambda: conv_case(8, 32, 32, 640, 640, up=True, stats=True),
     "conv3_upsample_640_ph": lambda: conv_case(8, 32, 32, 640, 640, up=True, stats=True, phases=True),
     "conv3_upsample_1280": lambda: conv_case(8, 16, 16, 1280, 1280, up=True, stats=True),

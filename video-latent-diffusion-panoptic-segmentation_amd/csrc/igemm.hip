@@ -794,7 +794,7 @@ template <int W, int R> struct Geo {
 };
 }  // namespace halo
 
-template <int W, int R>
+template <int W, int R, bool SPLIT>
 __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
   using namespace halo;
   typedef bf16_t T;
@@ -822,15 +822,18 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
   }
   // split-K over channel blocks (the 16x16 level's whole-image tiles): split `split` of ksplit
   // runs channel blocks [cb0, cb1) and writes an fp32 partial slab; a tile's splits are adjacent ids
-  const int split = tile % p.ksplit;
-  tile /= p.ksplit;
+  // (SPLIT = false: the unsplit instantiation carries no split-K code — it costs the 64x64-level
+  // kernel registers it does not have to spare)
+  const int ksplit = SPLIT ? p.ksplit : 1;
+  const int split = SPLIT ? tile % ksplit : 0;
+  tile /= ksplit;
   int tm, tn;
   grouped_tile(tile, p.M / BM, p.tiles_n, p.group_m, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
   const int b = m0 / p.hw_out;
   const int oy0 = (m0 - b * p.hw_out) / W;
   const int ncb_all = p.cin / 64;
-  const int cb0 = ncb_all * split / p.ksplit, cb1 = ncb_all * (split + 1) / p.ksplit;
+  const int cb0 = SPLIT ? ncb_all * split / ksplit : 0, cb1 = SPLIT ? ncb_all * (split + 1) / ksplit : ncb_all;
   const int nsteps = 9 * (cb1 - cb0);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -976,7 +979,7 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
     }
     __syncthreads();
     const int mh = m0 + h * EPI_ROWS;
-    if (p.ksplit > 1) {
+    if (SPLIT && ksplit > 1) {
       write_partial_rows<EPI_ROWS, BN, NT>(p, p.partial + (int64_t)split * p.M * p.n, mh, n0, stage, PITCH);
       continue;
     }
@@ -989,16 +992,24 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
 // the kernel is instantiated for, whole output rows per tile
 int g_halo_mode = 0;   // tuning hook: 0 planner, 1 never, 2 whenever legal
 int g_epi_pre = 1;     // tuning hook: bf16 pre-activated staging epilogue (1) or fp32 staging (0)
-// output rows per halo tile: 4 at widths 64 / 32, the whole image at 16 (the 16x16 level, split
-// over channel blocks)
-constexpr int halo_rows(int w) { return w == 64 ? 4 : (w == 32 ? 4 : (w == 16 ? 16 : 0)); }
+// output rows per halo tile: 4 at width 64; at 32, 8 (256-row tiles split over channel blocks) for
+// >= 1280 input channels, else 4; the whole image at 16 (the 16x16 level, split over channel
+// blocks).  opbench at B = 8, 32x32 level, us: [1280 || 640] -> 640 196.5 (128x160 x 2 tiles) ->
+// 173.4, [640 || 640] -> 640 139.7 -> 124.9; but 640 -> 640 80.2 vs 79.5, 320 -> 640 47.0 vs 50.2,
+// [640 || 320] -> 640 111.8 vs 131.8 (4-row tiles)
+int g_halo32_rows = 0;   // tuning hook (ldm_conv2d_set_halo_rows32): 0 planner, 4 or 8 forced
+int halo_rows(int w, int cin) {
+  if (w == 32) return g_halo32_rows ? g_halo32_rows : (cin >= 1280 ? 8 : 4);
+  return w == 64 ? 4 : (w == 16 ? 16 : 0);
+}
 bool halo_legal(const ldm_conv_params* q, int es) {
   if (es != 2 || q->ksize != 3 || q->stride != 1 || q->upsample || q->pad_mode != 0) return false;
   if (q->c0 % 64 || q->c1 % 64 || q->kpad != 9 * (q->c0 + q->c1)) return false;
   if (q->h_in != q->h_out || q->w_in != q->w_out) return false;
   if (q->out_layout != LDM_OUT_NHWC || q->out_f32) return false;
   const int W = q->w_out;
-  return halo_rows(W) && q->h_out % halo_rows(W) == 0;
+  const int rows = halo_rows(W, q->c0 + q->c1);
+  return rows && q->h_out % rows == 0;
 }
 
 template <typename T>
@@ -1006,11 +1017,16 @@ void launch_splitk_epilogue(const ConvArgs& a, hipStream_t s);
 
 int launch_halo(ConvArgs a, hipStream_t s) {
   a.tiles_n = (a.n + halo::BN - 1) / halo::BN;
-  const int bm = a.w_out * halo_rows(a.w_out);
+  const int bm = a.w_out * halo_rows(a.w_out, a.cin);
   a.nblk = (a.M / bm) * a.tiles_n * a.ksplit;
-  if (a.w_out == 64) hipLaunchKernelGGL((conv3_halo_kernel<64, 4>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
-  else if (a.w_out == 32) hipLaunchKernelGGL((conv3_halo_kernel<32, 4>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
-  else hipLaunchKernelGGL((conv3_halo_kernel<16, 16>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  const bool sp = a.ksplit > 1;
+  if (a.w_out == 64) hipLaunchKernelGGL((conv3_halo_kernel<64, 4, false>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  else if (a.w_out == 32 && bm == 256 && sp)
+    hipLaunchKernelGGL((conv3_halo_kernel<32, 8, true>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  else if (a.w_out == 32 && bm == 256) hipLaunchKernelGGL((conv3_halo_kernel<32, 8, false>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  else if (a.w_out == 32) hipLaunchKernelGGL((conv3_halo_kernel<32, 4, false>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  else if (sp) hipLaunchKernelGGL((conv3_halo_kernel<16, 16, true>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
+  else hipLaunchKernelGGL((conv3_halo_kernel<16, 16, false>), dim3(a.nblk), dim3(halo::NT), 0, s, a);
   LDM_CHECK_LAUNCH();
   if (a.ksplit > 1) launch_splitk_epilogue<bf16_t>(a, s);
   return LDM_OK;
@@ -1332,12 +1348,12 @@ int g_halo_split = 0;   // tuning hook (ldm_conv2d_set_halo_split): force the 16
 int halo_plan(const ldm_conv_params* q, int es, bool mixed) {
   if (g_halo_mode == 1 || mixed || g_force_bm || !halo_legal(q, es)) return 0;
   const int ncb = (q->c0 + q->c1) / 64;
-  if (q->w_out == 16) {
+  if (q->w_out == 16 || (q->w_out == 32 && halo_rows(32, q->c0 + q->c1) == 8)) {
     // whole 16x16 images (256 rows) x 160 channels, K split over channel blocks toward >= 256 blocks
     // with >= 4 channel blocks per split (opbench, B = 8, 16x16 level, us incl. the split-K
     // reduction, halo vs 128x160 x 4 tiles: 1280 -> 1280 76.0 vs 79.3, [1280 || 1280] -> 1280 123.6
     // vs 134.5; but 640 -> 1280 at 5 splits of 2 channel blocks 70.9 vs 51.8)
-    const int64_t base = (int64_t)q->batch * (q->n / halo::BN);
+    const int64_t base = (int64_t)q->batch * (q->h_out / halo_rows(q->w_out, q->c0 + q->c1)) * (q->n / halo::BN);
     if (q->n % halo::BN) return 0;
     if (g_halo_split > 0) return std::min(g_halo_split, ncb);
     for (int ks = 1; ks <= ncb; ++ks)
@@ -1370,6 +1386,7 @@ int g_group_m = 8;
 extern "C" void ldm_conv2d_set_raster_group(int g) { g_group_m = g >= 1 ? g : 8; }
 extern "C" void ldm_conv2d_set_halo(int mode) { g_halo_mode = (mode == 1 || mode == 2) ? mode : 0; }
 extern "C" void ldm_conv2d_set_halo_split(int ks) { g_halo_split = ks > 0 ? ks : 0; }
+extern "C" void ldm_conv2d_set_halo_rows32(int rows) { g_halo32_rows = (rows == 4 || rows == 8) ? rows : 0; }
 extern "C" void ldm_conv2d_set_ars(int mode) { g_ars_mode = (mode >= 1 && mode <= 3) ? mode : 0; }
 extern "C" void ldm_conv2d_set_splitk_cols(int cols) { g_splitk_cols = (cols == 64 || cols == 128) ? cols : 0; }
 extern "C" void ldm_conv2d_set_epilogue(int mode) { g_epi_pre = mode == 1 ? 0 : 1; }
@@ -1402,7 +1419,7 @@ extern "C" int ldm_conv2d_describe_plan(const ldm_conv_params* q, int* out) {
   const bool ars = !halo && !wbm && use_ars(q, es, mixed, M);
   if (halo || wbm || ars) {
     out[0] = halo ? 1 : (wbm ? 2 : 3);
-    out[1] = halo ? q->w_out * halo_rows(q->w_out) : wbm;
+    out[1] = halo ? q->w_out * halo_rows(q->w_out, q->c0 + q->c1) : wbm;
     out[2] = halo ? halo::BN : (wbm ? 320 : 0);
     out[3] = halo ? hks : 1;
     out[4] = 0;

@@ -72,6 +72,7 @@ EXPORTS = {
     "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_conv2d_set_halo": (None, [_i]),
     "ldm_conv2d_set_halo_split": (None, [_i]),
+    "ldm_conv2d_set_halo_rows32": (None, [_i]),
     "ldm_conv2d_set_ars": (None, [_i]),
     "ldm_conv2d_set_wide": (None, [_i]),
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
@@ -658,6 +659,13 @@ def set_conv_halo(mode=0):
 def set_conv_halo_split(ks=0):
     """Tuning hook: split-K factor of the 16x16 whole-image halo tiles (0 = planner)."""
     load_library().ldm_conv2d_set_halo_split(int(ks))
+
+
+def set_conv_halo_rows32(rows=0):
+    """Tuning / A-B hook: output rows per halo tile at the 32x32 level: 0 the planner (8 for >= 1280
+    input channels, else 4), 4 or 8 forced (8: 256-row tiles, K split over channel blocks as at the
+    16x16 level)."""
+    load_library().ldm_conv2d_set_halo_rows32(int(rows))
 
 
 def set_conv_ars(mode=0):
