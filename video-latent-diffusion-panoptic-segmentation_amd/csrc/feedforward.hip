@@ -217,7 +217,7 @@ __device__ __forceinline__ void proj_out_tile(const ConvArgs& p2, const ConvArgs
   __syncthreads();
   int tid_late = tid;
   asm volatile("" : "+v"(tid_late));
-  epilogue_fast<BM, C, NT, true>(p3, m0, 0, stg, HP, reinterpret_cast<float*>(smem) + BM * HP / 2, tid_late);
+  epilogue_fast<BM, C, NT, true, false>(p3, m0, 0, stg, HP, reinterpret_cast<float*>(smem) + BM * HP / 2, tid_late);
   __syncthreads();
 }
 
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(512, 1) void feedforward_kernel(const ConvArgs g1, 
     // keep a step's W fragments in flight
     int tid_late = tid;
     asm volatile("" : "+v"(tid_late));
-    epilogue_fast<BM, C, NT, true>(p2, m0, 0, stg, HP, reinterpret_cast<float*>(smem) + BM * HP / 2, tid_late);
+    epilogue_fast<BM, C, NT, true, false>(p2, m0, 0, stg, HP, reinterpret_cast<float*>(smem) + BM * HP / 2, tid_late);
     __syncthreads();   // the next tile's x loads / stages reuse LDS
   }
 }

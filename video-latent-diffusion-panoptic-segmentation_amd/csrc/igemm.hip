@@ -983,8 +983,8 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
       write_partial_rows<EPI_ROWS, BN, NT>(p, p.partial + (int64_t)split * p.M * p.n, mh, n0, stage, PITCH);
       continue;
     }
-    if (fast && fast_temb_ok(p, mh, EPI_ROWS)) epilogue_fast<EPI_ROWS, BN, NT>(p, mh, n0, stage, PITCH, red);
-    else epilogue_rows<T, EPI_ROWS, BN, NT>(p, mh, n0, raw, red);
+    if (fast && fast_temb_ok(p, mh, EPI_ROWS)) epilogue_fast<EPI_ROWS, BN, NT, false, false>(p, mh, n0, stage, PITCH, red);
+    else epilogue_rows<T, EPI_ROWS, BN, NT, false>(p, mh, n0, raw, red);
   }
 }
 

@@ -42,8 +42,10 @@ struct ConvArgs {
 // Storage row of GEMM row m: m itself, or in phase mode (rows ordered (b, phase (dy, dx), y, x) over
 // the h_in x w_in input grid) the output pixel (b, 2y + dy, 2x + dx) of the 2x upsampled image —
 // batch-major either way, so m / hw_out is the batch in both.
+// (PH = false: a kernel that never runs the phase form drops the remap — it costs registers)
+template <bool PH = true>
 __device__ __forceinline__ int64_t out_row(const ConvArgs& p, int m) {
-  if (!p.phase) return m;
+  if (!PH || !p.phase) return m;
   const int hwl = p.hw_out >> 2, wl = p.w_out >> 1;
   const int b = m / p.hw_out, r = m - b * p.hw_out;
   const int ph = r / hwl, q = r - ph * hwl;
@@ -199,7 +201,7 @@ __device__ __forceinline__ void load4(const char* base, int64_t idx, float* v) {
 // Finish 4 consecutive output channels [n, n+4) of row m from raw accumulators: + bias,
 // + time embedding (both preloaded by the caller: they depend only on the column / batch),
 // activation, + residual (NHWC: preloaded into `res`), store.  `v` returns the stored values.
-template <typename T>
+template <typename T, bool PH = true>
 __device__ __forceinline__ void finish4(const ConvArgs& p, int b, int pix, int m, int n, float* v,
                                         const float* bias4, const float* temb4, const float* res) {
   const int N = p.n;
@@ -220,7 +222,7 @@ __device__ __forceinline__ void finish4(const ConvArgs& p, int b, int pix, int m
   }
   int64_t idx;
   if (p.out_layout == LDM_OUT_NHWC) {
-    idx = out_row(p, m) * N + n;
+    idx = out_row<PH>(p, m) * N + n;
     if (p.residual) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] += res[r];
@@ -327,7 +329,7 @@ __device__ __forceinline__ void gn_units_out(const ConvArgs& p, int m0, int n0, 
 // With gn_part set, per-channel (sum, sumsq) over each 64-row chunk of the stored values
 // is reduced through `red` ([RP][CW][ROWS/64][4][2] floats) and added to the chunk's batch
 // accumulators in gn_part (fp64 atomics; a chunk never spans two batches: hw % 64 == 0).
-template <typename T, int ROWS, int COLS, int NT, typename RawFn>
+template <typename T, int ROWS, int COLS, int NT, bool PH = true, typename RawFn>
 __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0, RawFn raw, float* red) {
   constexpr int CW = COLS / 4;           // chunks per row
   constexpr int RP = NT / CW;            // rows per pass
@@ -406,7 +408,7 @@ __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0,
         if (q0 + q >= NP || r >= ROWS || m0 + r >= p.M) continue;
         raw(r, c4, v[q]);
         if (nhwc_res) {
-          const int64_t idx = out_row(p, m0 + r) * N + n;
+          const int64_t idx = out_row<PH>(p, m0 + r) * N + n;
           if (n + 3 < N) {
             load4<T>(p.residual, idx, rv[q]);
           } else {
@@ -425,7 +427,7 @@ __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0,
 #pragma unroll
           for (int k = 0; k < 4; ++k) temb4[k] = p.temb[(int64_t)tb * p.temb_stride + min(n + k, N - 1)];
         }
-        finish4<T>(p, bq[q], pq[q], m0 + r, n, v[q], bias4, temb4, rv[q]);
+        finish4<T, PH>(p, bq[q], pq[q], m0 + r, n, v[q], bias4, temb4, rv[q]);
         if (stats) {
           const int hh = HALVES > 1 ? (r >> 6) : 0;
 #pragma unroll
@@ -520,7 +522,7 @@ __device__ __forceinline__ bool fast_temb_ok(const ConvArgs& p, int m0, int rows
 // PRE: the staged tile already holds the final pre-residual values as bf16 (bias, time
 // embedding and activation applied from the accumulators by the caller, `pitch` in bf16
 // elements); only the residual, the stores and the GroupNorm statistics are left.
-template <int ROWS, int COLS, int NT, bool PRE = false>
+template <int ROWS, int COLS, int NT, bool PRE = false, bool PH = true>
 __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0, const void* stage_v, int pitch,
                                               float* red, int tid_in = -1) {
   const int tid = tid_in >= 0 ? tid_in : (int)threadIdx.x;
@@ -613,7 +615,7 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
       for (int q = 0; q < GP; ++q) {
         const int r = r0 + (q0 + q) * RP;
         if (res && q0 + q < NP && r < ROWS && m0 + r < p.M)
-          rv[q] = *reinterpret_cast<const uint4*>(res + out_row(p, m0 + r) * N + n);
+          rv[q] = *reinterpret_cast<const uint4*>(res + out_row<PH>(p, m0 + r) * N + n);
       }
 #pragma unroll
       for (int q = 0; q < GP; ++q) {
@@ -651,7 +653,7 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
 #ifdef LDM_ABL_EPI_NO_STORE   // ablation build: the epilogue's math kept, its global stores dropped
         if (packed.x == 0x12345678u && packed.y == 0x9abcdef0u) *reinterpret_cast<uint4*>(out + (int64_t)m * N + n) = packed;
 #else
-        *reinterpret_cast<uint4*>(out + out_row(p, m) * N + n) = packed;
+        *reinterpret_cast<uint4*>(out + out_row<PH>(p, m) * N + n) = packed;
 #endif
         if (stats) {
           float st[8];
