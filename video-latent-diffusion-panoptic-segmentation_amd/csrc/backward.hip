@@ -111,8 +111,19 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
   const char* sbase = reinterpret_cast<const char*>(smem);
 
-  const int split = blockIdx.x % p.splits;
-  const int tile = blockIdx.x / p.splits;
+  // XCD-contiguous ids (block b runs on XCD b mod 8), tiles fastest: an XCD works through one or two
+  // M ranges (splits) for all of their output tiles, so their dy / x rows are shared in its L2.
+  // (split fastest spread every XCD over all splits whenever splits != 8: L2 hit rate 0.21 / 0.51,
+  // 1.4 / 2.9 GB fetched for the GEGLU 320 / up-block 960 weight gradients, r04k PMC)
+  int split, tile;
+  {
+    const int bid = blockIdx.x, nblk = gridDim.x;
+    const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
+    const int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    const int ntile = nblk / p.splits;
+    split = t / ntile;
+    tile = t - split * ntile;
+  }
   const int tn = tile % p.tiles_n, tk = tile / p.tiles_n;
   const int n0 = tn * TE, k0 = tk * TE;
   const int m_lo = (int)((int64_t)p.M * split / p.splits);
