@@ -329,6 +329,29 @@ __device__ __forceinline__ void gn_units_out(const ConvArgs& p, int m0, int n0, 
 // With gn_part set, per-channel (sum, sumsq) over each 64-row chunk of the stored values
 // is reduced through `red` ([RP][CW][ROWS/64][4][2] floats) and added to the chunk's batch
 // accumulators in gn_part (fp64 atomics; a chunk never spans two batches: hw % 64 == 0).
+// GroupNorm statistics of one stored row into the thread's per-64-row-half accumulators.  The row
+// r = r0 + rq (r0 < RP, rq = the unrolled pass's row offset) lies in half rq >> 6 unless its pass
+// straddles a 64-row boundary; the half is resolved at compile time wherever it can be (a runtime
+// index into s[HALVES][..] expands into a v_cmp / v_cndmask chain over every accumulator: ~460
+// selects per thread in the halo conv's epilogue), and by one select per value where it cannot.
+template <int HALVES, int NK, int RP>
+__device__ __forceinline__ void stats_add(float (&s)[HALVES][NK], float (&sq)[HALVES][NK], int rq, int r,
+                                          const float* x) {
+  const int hlo = (rq >> 6) < HALVES - 1 ? (rq >> 6) : HALVES - 1;
+  const int hhi = ((rq + RP - 1) >> 6) < HALVES - 1 ? ((rq + RP - 1) >> 6) : HALVES - 1;
+#pragma unroll
+  for (int h = 0; h < HALVES; ++h) {
+    if (h < hlo || h > hhi) continue;            // (compile-time after unrolling)
+    const bool mine = hlo == hhi || (h == hlo ? r < 64 * hhi : r >= 64 * hhi);
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      const float v = mine ? x[k] : 0.f;
+      s[h][k] += v;
+      sq[h][k] = fmaf(v, v, sq[h][k]);
+    }
+  }
+}
+
 template <typename T, int ROWS, int COLS, int NT, bool PH = true, typename RawFn>
 __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0, RawFn raw, float* red) {
   constexpr int CW = COLS / 4;           // chunks per row
@@ -429,14 +452,11 @@ __device__ __forceinline__ void epilogue_rows(const ConvArgs& p, int m0, int n0,
         }
         finish4<T, PH>(p, bq[q], pq[q], m0 + r, n, v[q], bias4, temb4, rv[q]);
         if (stats) {
-          const int hh = HALVES > 1 ? (r >> 6) : 0;
+          // statistics of the value as stored (bf16-rounded on the bf16 path)
+          float x[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            // statistics of the value as stored (bf16-rounded on the bf16 path)
-            const float x = (sizeof(T) == 2 && !p.out_f32) ? bf2f(f2bf(v[q][k])) : v[q][k];
-            s[hh][k] += x;
-            sq[hh][k] += x * x;
-          }
+          for (int k = 0; k < 4; ++k) x[k] = (sizeof(T) == 2 && !p.out_f32) ? bf2f(f2bf(v[q][k])) : v[q][k];
+          stats_add<HALVES, 4, RP>(s, sq, (q0 + q) * RP, r, x);
         }
       }
     }
@@ -658,9 +678,7 @@ __device__ __forceinline__ void epilogue_fast(const ConvArgs& p, int m0, int n0,
         if (stats) {
           float st[8];
           unpack8(packed, st);                   // statistics of the value as stored
-          const int hh = HALVES > 1 ? (r >> 6) : 0;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) { s[hh][k] += st[k]; sq[hh][k] += st[k] * st[k]; }
+          stats_add<HALVES, 8, RP>(s, sq, (q0 + q) * RP, r, st);
         }
         if (PRE && p.row_stats) {
           float st[8];
