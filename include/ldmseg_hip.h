@@ -466,6 +466,9 @@ int ldm_conv2d_wgrad(const ldm_wgrad_params* p, ldm_stream_t stream);
 /* Tuning / A-B hook: 1 (default) runs the bf16 weight gradient on a ring of four 32-pixel LDS
  * stages (three in flight), 0 on two 64-pixel stages. */
 void ldm_conv2d_wgrad_set_ring(int ring);
+/* A-B hook: 1 (default) = stride-1 weight gradients load their operands by per-lane pointers
+ * advanced 16 rows per DMA (branch-free); 0 = the general pixel-decoding loader everywhere. */
+void ldm_conv2d_wgrad_set_fast_loader(int on);
 
 /* ldm_colsum — out[s][c] (+)= sum over the rows of segment s of x[rows][c] (segments split the
  * rows evenly).  Bias gradients (1 segment) and per-batch time-embedding gradients (batch

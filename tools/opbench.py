@@ -65,7 +65,7 @@ def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scal
     return run, 4.0 * B * heads * N * N * (C // heads), None
 
 
-def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False, ring=True):
+def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False, ring=True, fast=True):
     g = torch.Generator(device=DEV).manual_seed(0)
     x = torch.randn(B, H, W, Cin, device=DEV, generator=g).to(BF)
     dy = torch.randn(B, H, W, Cout, device=DEV, generator=g).to(BF)
@@ -75,6 +75,7 @@ def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False, ring=True):
 
     def run():
         K.set_wgrad_ring(ring)
+        K.set_wgrad_fast_loader(fast)
         return K.conv2d_wgrad(pc, x, B, H, W, dy, dw=dw)
     return run, 2.0 * B * H * W * Cout * k * k * Cin, None
 
@@ -284,6 +285,15 @@ CASES = {
     "wgrad_ff2_1280": lambda: wgrad_case(16, 64, 64, 1280, 320, k=1),
     "wgrad_proj_320": lambda: wgrad_case(16, 64, 64, 320, 320, k=1),
     "wgrad_qkv_320": lambda: wgrad_case(16, 64, 64, 320, 960, k=1),
+    "wgrad_l0_320_gen": lambda: wgrad_case(16, 64, 64, 320, 320, fast=False),
+    "wgrad_l1_640_gen": lambda: wgrad_case(16, 32, 32, 640, 640, fast=False),
+    "wgrad_l2_1280_gen": lambda: wgrad_case(16, 16, 16, 1280, 1280, fast=False),
+    "wgrad_l3_1280_gen": lambda: wgrad_case(16, 8, 8, 1280, 1280, fast=False),
+    "wgrad_up_960_gen": lambda: wgrad_case(16, 64, 64, 960, 320, fast=False),
+    "wgrad_geglu_320_gen": lambda: wgrad_case(16, 64, 64, 320, 2560, k=1, geglu=True, fast=False),
+    "wgrad_ff2_1280_gen": lambda: wgrad_case(16, 64, 64, 1280, 320, k=1, fast=False),
+    "wgrad_proj_320_gen": lambda: wgrad_case(16, 64, 64, 320, 320, k=1, fast=False),
+    "wgrad_qkv_320_gen": lambda: wgrad_case(16, 64, 64, 320, 960, k=1, fast=False),
     "wgrad_l0_320_old": lambda: wgrad_case(16, 64, 64, 320, 320, ring=False),
     "wgrad_l1_640_old": lambda: wgrad_case(16, 32, 32, 640, 640, ring=False),
     "wgrad_l2_1280_old": lambda: wgrad_case(16, 16, 16, 1280, 1280, ring=False),

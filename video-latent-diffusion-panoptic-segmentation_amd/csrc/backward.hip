@@ -100,7 +100,14 @@ __device__ __forceinline__ Frag8<float> wg_frag<float>(const char* img, int r0, 
 // us, MFMAs removed 410 -> 364 us at the 64x64-level 3x3 320): with one 32-KB 64-pixel stage in
 // flight per block (NS = 2) every stage waits out a memory round trip.  The bf16 default is a ring of
 // four 32-pixel stages (16 KB each, three in flight, counted vmcnt and a raw barrier per stage).
-template <typename T, int MB, int NS>
+// Loader modes (block-uniform, chosen on the host): WG_GENERAL walks (b, y, x) and decodes every
+// source pixel (stride 2, upsample); WG_1X1 (1x1, stride 1) and WG_PLAIN (k x k, stride 1, same
+// size, 16 / w_out < h_out) keep one pointer per operand that advances by 16 rows per DMA and test
+// the tap's bounds with a wrap-by-one-subtraction (x, y) walker: straight-line selects, no
+// divergent branches (the branchy general form cost 6.7 VALU + 5.6 SALU per MFMA, r04k PMC).
+enum { WG_GENERAL = 0, WG_1X1 = 1, WG_PLAIN = 2 };
+
+template <typename T, int MB, int NS, int MODE = WG_GENERAL>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
   constexpr int ES = sizeof(T), EPC = 16 / ES;
   constexpr int TE = 256 / ES, WT = TE / 2, NF = WT / 16;
@@ -162,6 +169,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
   // plain: source pixel = m + (ky - pad) * w_in + (kx - pad) (valid only when in bounds)
   const int pix_shift = (ky - p.pad) * p.w_in + (kx - p.pad);
   int mrow = m_lo + rlow;
+  // fast modes: per-lane operand pointers (unused lanes are redirected to kZero16 by a select)
+  const char* dyp = p.dy + ((int64_t)mrow * p.n + ncol) * ES;
+  const char* xp = reinterpret_cast<const char*>(xs + ((int64_t)mrow + (MODE == WG_PLAIN ? pix_shift : 0)) * cs + cof);
+  const int64_t dystep = (int64_t)16 * p.n * ES, xstep = (int64_t)16 * cs * ES;
+  const int dyk = ky - p.pad, dxk = kx - p.pad;
   auto issue = [&](int mb, int slot) {
     (void)mb;
 #ifdef LDM_ABL_NO_LOADS
@@ -169,6 +181,31 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
 #endif
     const unsigned dyb = lds0 + (unsigned)(slot * 2 * IMG);
     const unsigned xb = dyb + IMG;
+    if constexpr (MODE != WG_GENERAL) {
+#pragma unroll
+      for (int i = 0; i < MB / 16; ++i) {
+        const bool mok = mrow < m_hi;
+        bool xok = mok && kval;
+        if constexpr (MODE == WG_PLAIN)
+          xok = xok && (unsigned)(wy + dyk) < (unsigned)p.h_in && (unsigned)(wx + dxk) < (unsigned)p.w_in;
+        const void* sd = (mok && nval) ? (const void*)dyp : (const void*)&kZero16;
+        const void* sx = xok ? (const void*)xp : (const void*)&kZero16;
+        const unsigned off = (unsigned)((16 * i + 4 * wave) * 256);
+        glds16(sd, __builtin_amdgcn_readfirstlane(dyb + off));
+        glds16(sx, __builtin_amdgcn_readfirstlane(xb + off));
+        mrow += 16;
+        dyp += dystep;
+        xp += xstep;
+        if constexpr (MODE == WG_PLAIN) {
+          wx += r16;
+          const int c = wx >= p.w_out;
+          wx -= c ? p.w_out : 0;
+          wy += q16 + c;
+          wy -= wy >= p.h_out ? p.h_out : 0;
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < MB / 16; ++i) {
       const int m = mrow;
@@ -961,10 +998,26 @@ int lnb_launch(const void* x, const void* dy, int rows, int c, const float* gamm
 
 size_t round16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+// Pixel-axis splits: the makespan in block-work units, per XCD (blocks go round-robin to the 8 XCDs;
+// 32 CUs x 2 resident blocks each), divided by the splits (a block's work is M / splits).  A round of
+// two blocks per CU costs 2 units, a last partial round of at most one block per CU ~1.6 (a lone
+// block issues faster).  The old rule (>= 512 blocks) left e.g. 552 blocks for the 3x3 320 at 64x64
+// (69 tiles x 8): a second round of 40 lone blocks, ~45 % of the kernel.  Each split adds a
+// [n][kpad] fp32 slab to write and reduce: ~33 ns per tile at HBM rate against ~9 ns per pixel
+// row for one unit, i.e. 3.7 tiles / M units per split.
 int wgrad_splits(const ldm_wgrad_params* q, int M, int tiles) {
-  const int max_by_rows = std::max(1, M / 256);
-  int sp = (512 + tiles - 1) / tiles;
-  return std::max(1, std::min(std::min(sp, max_by_rows), 64));
+  (void)q;
+  const int max_sp = std::max(1, std::min(M / 256, 64));
+  int best = 1;
+  double best_cost = 1e30;
+  for (int sp = 1; sp <= max_sp; ++sp) {
+    const int per_xcd = (tiles * sp + 7) / 8;
+    const int full = per_xcd / 64, rem = per_xcd % 64;
+    const double units = 2.0 * full + (rem == 0 ? 0.0 : rem > 32 ? 2.0 : 1.6);
+    const double cost = units / sp + sp * 3.7 * tiles / M;
+    if (cost < best_cost) { best_cost = cost; best = sp; }
+  }
+  return best;
 }
 
 int wgrad_validate(const ldm_wgrad_params* q, int* es_out, int* M_out) {
@@ -998,8 +1051,10 @@ int wgrad_validate(const ldm_wgrad_params* q, int* es_out, int* M_out) {
 
 namespace {
 int g_wgrad_ring = 1;   // tuning / A-B hook (ldm_conv2d_wgrad_set_ring): 0 = two 64-pixel stages
+int g_wgrad_fast = 1;   // A-B hook (ldm_conv2d_wgrad_set_fast_loader): 0 = the general loader everywhere
 }  // namespace
 extern "C" void ldm_conv2d_wgrad_set_ring(int ring) { g_wgrad_ring = ring ? 1 : 0; }
+extern "C" void ldm_conv2d_wgrad_set_fast_loader(int on) { g_wgrad_fast = on ? 1 : 0; }
 
 extern "C" size_t ldm_conv2d_wgrad_workspace_bytes(const ldm_wgrad_params* q) {
   int es = 0, M = 0;
@@ -1033,7 +1088,15 @@ extern "C" int ldm_conv2d_wgrad(const ldm_wgrad_params* q, ldm_stream_t stream) 
   a.part = static_cast<float*>(q->workspace);
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int blocks = tiles_n * tiles_k * sp;
-  if (q->dtype == LDM_BF16 && g_wgrad_ring) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 32, 4>), dim3(blocks), dim3(256), 0, s, a);
+  const bool plain = q->stride == 1 && !q->upsample && q->h_in == q->h_out && q->w_in == q->w_out;
+  const int mode = !g_wgrad_fast || !plain ? WG_GENERAL
+                   : q->ksize == 1          ? WG_1X1
+                   : 16 / q->w_out < q->h_out ? WG_PLAIN : WG_GENERAL;
+  if (q->dtype == LDM_BF16 && g_wgrad_ring && mode == WG_1X1)
+    hipLaunchKernelGGL((wgrad_kernel<bf16_t, 32, 4, WG_1X1>), dim3(blocks), dim3(256), 0, s, a);
+  else if (q->dtype == LDM_BF16 && g_wgrad_ring && mode == WG_PLAIN)
+    hipLaunchKernelGGL((wgrad_kernel<bf16_t, 32, 4, WG_PLAIN>), dim3(blocks), dim3(256), 0, s, a);
+  else if (q->dtype == LDM_BF16 && g_wgrad_ring) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 32, 4>), dim3(blocks), dim3(256), 0, s, a);
   else if (q->dtype == LDM_BF16) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 64, 2>), dim3(blocks), dim3(256), 0, s, a);
   else hipLaunchKernelGGL((wgrad_kernel<float, 64, 2>), dim3(blocks), dim3(256), 0, s, a);
   LDM_CHECK_LAUNCH();

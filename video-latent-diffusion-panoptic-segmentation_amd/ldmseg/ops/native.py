@@ -103,6 +103,7 @@ EXPORTS = {
     "ldm_attention_set_qs2": (None, [_i]),
     "ldm_attention_set_bwd32": (None, [_i]),
     "ldm_conv2d_wgrad_set_ring": (None, [_i]),
+    "ldm_conv2d_wgrad_set_fast_loader": (None, [_i]),
     "ldm_attention_set_waves": (None, [_i]),
     "ldm_attention_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_bwd": (_i, [ctypes.POINTER(AttnParams), _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
@@ -616,6 +617,12 @@ def set_attention_fp8_scaled(enabled=True):
 def set_wgrad_ring(ring=True):
     """Tuning / A-B hook: bf16 weight gradient on four 32-pixel LDS stages (default) or two 64-pixel."""
     load_library().ldm_conv2d_wgrad_set_ring(int(bool(ring)))
+
+
+def set_wgrad_fast_loader(enabled=True):
+    """A-B hook: the weight gradient's pointer-walk operand loader for stride-1 convs (default) or
+    the general pixel-decoding loader everywhere."""
+    load_library().ldm_conv2d_wgrad_set_fast_loader(int(bool(enabled)))
 
 
 def set_attention_bwd32(enabled=True):
