@@ -464,7 +464,7 @@ typedef struct {
 size_t ldm_conv2d_wgrad_workspace_bytes(const ldm_wgrad_params* p);
 int ldm_conv2d_wgrad(const ldm_wgrad_params* p, ldm_stream_t stream);
 /* Tuning / A-B hook: 1 (default) runs the bf16 weight gradient on a ring of four 32-pixel LDS
- * stages (three in flight), 0 on two 64-pixel stages. */
+ * stages (three in flight), 0 on two 64-pixel stages, 2 on five 32-pixel stages (stride-1 convs). */
 void ldm_conv2d_wgrad_set_ring(int ring);
 /* A-B hook: 1 (default) = stride-1 weight gradients load their operands by per-lane pointers
  * advanced 16 rows per DMA (branch-free); 0 = the general pixel-decoding loader everywhere. */
@@ -473,7 +473,7 @@ void ldm_conv2d_wgrad_set_fast_loader(int on);
 /* ldm_colsum — out[s][c] (+)= sum over the rows of segment s of x[rows][c] (segments split the
  * rows evenly).  Bias gradients (1 segment) and per-batch time-embedding gradients (batch
  * segments).  geglu: columns are the packed GEGLU interleave, out is un-interleaved. fp32 out.
- * Deterministic: 256-row chunks write an fp32 slab (workspace, ldm_colsum_workspace_bytes)
+ * Deterministic: 128-row chunks write an fp32 slab (workspace, ldm_colsum_workspace_bytes)
  * that a second pass sums in chunk order — no atomics, bit-identical run to run. */
 size_t ldm_colsum_workspace_bytes(int rows, int c, int segments);
 int ldm_colsum(const void* x, int rows, int c, int segments, int geglu, float* out, int accumulate,

@@ -80,6 +80,33 @@ def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False, ring=True, fast=True):
     return run, 2.0 * B * H * W * Cout * k * k * Cin, None
 
 
+def colsum_case(rows, C, segments=1, geglu=False):
+    x = torch.randn(rows, C, device=DEV).to(BF)
+    out = torch.empty(segments, C, device=DEV)
+
+    def run():
+        return K.colsum(x, rows, C, segments, geglu=geglu, out=out)
+    return run, 0.0, 2.0 * rows * C
+
+
+def gn_bwd_case(B, HW, C, silu=True, add=True):
+    x = torch.randn(B, HW, C, device=DEV).to(BF)
+    dy = torch.randn(B, HW, C, device=DEV).to(BF)
+    gamma = torch.randn(C, device=DEV)
+    beta = torch.randn(C, device=DEV)
+    act = K.ACT_SILU if silu else K.ACT_NONE
+    _, mr = K.group_norm_train(x, B, HW, 32, gamma, beta, 1e-5, act=act)
+    a = torch.randn(B, HW, C, device=DEV).to(BF) if add else None
+    dx = torch.empty_like(x)
+    dg = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+
+    def run():
+        return K.group_norm_bwd(x, B, HW, 32, mr, gamma, beta, act, dy, add_src=a, dx0=dx, dgamma=dg, dbeta=db)
+    # algorithmic bytes: the partial pass reads x, dy; the apply pass reads x, dy (, add) and writes dx
+    return run, 0.0, (6 if add else 5) * x.numel() * 2.0
+
+
 def attn_bwd_case(B, N, C, heads=8, new=True):
     d = C // heads
     qkv = (torch.randn(B, N, 3 * C, device=DEV) * 0.5).to(BF)
@@ -276,6 +303,13 @@ CASES = {
     "attn_1024_d80_w8": lambda: attn_case(8, 1024, 640, waves=8),
     "attn_4096_d40_w4": lambda: attn_case(8, 4096, 320, waves=4),
     "attn_256_d160": lambda: attn_case(8, 256, 1280),
+    "colsum_l0_320": lambda: colsum_case(65536, 320),
+    "colsum_l0_320_seg16": lambda: colsum_case(65536, 320, 16),
+    "colsum_geglu_2560": lambda: colsum_case(65536, 2560, geglu=True),
+    "colsum_l2_1280": lambda: colsum_case(4096, 1280),
+    "gnb_l0_320": lambda: gn_bwd_case(16, 4096, 320),
+    "gnb_l0_960_noadd": lambda: gn_bwd_case(16, 4096, 960, add=False),
+    "gnb_l2_1280": lambda: gn_bwd_case(16, 256, 1280),
     "wgrad_l0_320": lambda: wgrad_case(16, 64, 64, 320, 320),
     "wgrad_l1_640": lambda: wgrad_case(16, 32, 32, 640, 640),
     "wgrad_l2_1280": lambda: wgrad_case(16, 16, 16, 1280, 1280),
@@ -294,6 +328,12 @@ CASES = {
     "wgrad_ff2_1280_gen": lambda: wgrad_case(16, 64, 64, 1280, 320, k=1, fast=False),
     "wgrad_proj_320_gen": lambda: wgrad_case(16, 64, 64, 320, 320, k=1, fast=False),
     "wgrad_qkv_320_gen": lambda: wgrad_case(16, 64, 64, 320, 960, k=1, fast=False),
+    "wgrad_l0_320_ns5": lambda: wgrad_case(16, 64, 64, 320, 320, ring=2),
+    "wgrad_l1_640_ns5": lambda: wgrad_case(16, 32, 32, 640, 640, ring=2),
+    "wgrad_l2_1280_ns5": lambda: wgrad_case(16, 16, 16, 1280, 1280, ring=2),
+    "wgrad_up_960_ns5": lambda: wgrad_case(16, 64, 64, 960, 320, ring=2),
+    "wgrad_geglu_320_ns5": lambda: wgrad_case(16, 64, 64, 320, 2560, k=1, geglu=True, ring=2),
+    "wgrad_qkv_320_ns5": lambda: wgrad_case(16, 64, 64, 320, 960, k=1, ring=2),
     "wgrad_l0_320_old": lambda: wgrad_case(16, 64, 64, 320, 320, ring=False),
     "wgrad_l1_640_old": lambda: wgrad_case(16, 32, 32, 640, 640, ring=False),
     "wgrad_l2_1280_old": lambda: wgrad_case(16, 16, 16, 1280, 1280, ring=False),

@@ -283,14 +283,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const WgArgs p) {
         __syncthreads();
       }
     } else {
-      static_assert(NS == 4, "ring depth");
+      static_assert(NS == 4 || NS == 5, "ring depth");
 #pragma unroll
       for (int i = 0; i < NS - 1; ++i)
         if (i < nst) issue(m_lo + i * MB, i);
       for (int st = 0; st < nst; ++st) {
-        // stage st landed for this wave; the (up to two) younger stages may stay in flight
+        // stage st landed for this wave; the (up to NS - 2) younger stages may stay in flight
         const int ahead = min(NS - 2, nst - 1 - st);
-        if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+        if (NS == 5 && ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory");
+        else if (ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
         else if (ahead == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // raw barrier (__syncthreads would drain the stages in flight): every wave's part of stage st
@@ -331,10 +332,10 @@ __device__ __forceinline__ int geglu_packed_row(int nt, int half) {
 __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ part, int splits, int n, int kpad,
                                                     int ksize, int cin_pad, int cin_real, int geglu,
                                                     float* __restrict__ dst, int accumulate) {
-  const int64_t total = (int64_t)n * kpad;
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int total = n * kpad;   // < 2^31 (checked by the launcher)
+  const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
-  const int np = (int)(idx / kpad), k = (int)(idx - (int64_t)np * kpad);
+  const int np = (int)((unsigned)idx / (unsigned)kpad), k = idx - np * kpad;
   const int taps = ksize * ksize;
   const int tap = k / cin_pad, c = k - tap * cin_pad;
   if (tap >= taps || c >= cin_real) return;
@@ -343,8 +344,17 @@ __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ pa
     const int blk = np >> 5, w = np & 31, half = n >> 1;
     nt = (w < 16) ? blk * 16 + w : half + blk * 16 + (w - 16);
   }
+  // the splits in order, eight loads in flight (a load-add loop waits out the latency per split)
   float s = 0.f;
-  for (int sp = 0; sp < splits; ++sp) s += part[(int64_t)sp * total + idx];
+  int sp = 0;
+  for (; sp + 8 <= splits; sp += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(sp + u) * total + idx];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; sp < splits; ++sp) s += part[(int64_t)sp * total + idx];
   const int64_t o = ((int64_t)nt * cin_real + c) * taps + tap;
   dst[o] = accumulate ? dst[o] + s : s;
 }
@@ -368,7 +378,20 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ x, in
   for (int e = 0; e < EPC; ++e) s[e] = 0.f;
   if (v < V) {
     const T* base = x + (int64_t)seg * rows_per_seg * C + v * EPC;
-    for (int r = r0 + ty; r < r1; r += 4) {
+    int r = r0 + ty;
+    // eight rows in flight per thread (a single-load loop waits out the memory latency per row)
+    for (; r + 28 < r1; r += 32) {
+      uint4 raw[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) raw[u] = *reinterpret_cast<const uint4*>(base + (int64_t)(r + 4 * u) * C);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const T* e = reinterpret_cast<const T*>(&raw[u]);
+#pragma unroll
+        for (int k = 0; k < EPC; ++k) s[k] += to_f(e[k]);
+      }
+    }
+    for (; r < r1; r += 4) {
       const uint4 raw = *reinterpret_cast<const uint4*>(base + (int64_t)r * C);
       const T* e = reinterpret_cast<const T*>(&raw);
 #pragma unroll
@@ -482,10 +505,7 @@ __global__ __launch_bounds__(256) void gnb_partial(const T* __restrict__ x0, con
       mean[k] = q.x; rstd[k] = q.y; gm[k] = gamma[cb + k]; bt[k] = beta[cb + k];
     }
     const int p0 = chunk * GNB_PPC, p1 = min(hw, p0 + GNB_PPC);
-    for (int pix = p0 + ty; pix < p1; pix += 4) {
-      const int64_t m = (int64_t)b * hw + pix;
-      const uint4 rx = load_cat(x0, x1, c0, c1, m, cb);
-      const uint4 rd = *reinterpret_cast<const uint4*>(dy + m * C + cb);
+    auto accum = [&](const uint4& rx, const uint4& rd) {
       const T* ex = reinterpret_cast<const T*>(&rx);
       const T* ed = reinterpret_cast<const T*>(&rd);
 #pragma unroll
@@ -496,6 +516,23 @@ __global__ __launch_bounds__(256) void gnb_partial(const T* __restrict__ x0, con
         s[k] += dz;
         sx[k] += dz * xh;
       }
+    };
+    int pix = p0 + ty;
+    // four pixels' loads in flight per thread, then the same sums in pixel order
+    for (; pix + 12 < p1; pix += 16) {
+      uint4 rx[4], rd[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t m = (int64_t)b * hw + pix + 4 * u;
+        rx[u] = load_cat(x0, x1, c0, c1, m, cb);
+        rd[u] = *reinterpret_cast<const uint4*>(dy + m * C + cb);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) accum(rx[u], rd[u]);
+    }
+    for (; pix < p1; pix += 4) {
+      const int64_t m = (int64_t)b * hw + pix;
+      accum(load_cat(x0, x1, c0, c1, m, cb), *reinterpret_cast<const uint4*>(dy + m * C + cb));
     }
   }
   __shared__ float red[4][64][EPC][2];
@@ -585,10 +622,13 @@ __global__ __launch_bounds__(256) void gnb_apply(const T* __restrict__ x0, const
                                                  int acc1) {
   constexpr int EPC = 16 / sizeof(T);
   const int C = c0 + c1, V = C / EPC, cpg = C / groups;
+  const bool vec = cpg >= EPC && !(reinterpret_cast<uintptr_t>(gamma) & 15) &&
+                   (act != LDM_ACT_SILU || !(reinterpret_cast<uintptr_t>(beta) & 15));
   for (int i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += gridDim.x * 256) {
-    const int64_t m = i / V;
-    const int cb = (int)(i - m * V) * EPC;
-    const int b = (int)(m / hw);
+    const int mi = (int)((unsigned)i / (unsigned)V);   // 32-bit: nvec < 2^31 (launcher)
+    const int64_t m = mi;
+    const int cb = (i - mi * V) * EPC;
+    const int b = (int)((unsigned)mi / (unsigned)hw);
     const uint4 rx = load_cat(x0, x1, c0, c1, m, cb);
     const uint4 rd = *reinterpret_cast<const uint4*>(dy + m * C + cb);
     const T* ex = reinterpret_cast<const T*>(&rx);
@@ -618,16 +658,44 @@ __global__ __launch_bounds__(256) void gnb_apply(const T* __restrict__ x0, const
     }
     uint4 res;
     T* r = reinterpret_cast<T*>(&res);
+    if (vec) {
+      // a vector spans at most two groups: both groups' statistics loaded once, selected per
+      // channel (no per-channel division or scalar stat loads); gamma / beta as vectors
+      const int gi0 = cb / cpg, bnd = (gi0 + 1) * cpg, gi1 = min(gi0 + 1, groups - 1);
+      const float2 q0 = mr[b * groups + gi0], q1 = mr[b * groups + gi1];
+      const float2 f0 = coef[b * groups + gi0], f1 = coef[b * groups + gi1];
+      float gm[EPC], bt[EPC];
 #pragma unroll
-    for (int k = 0; k < EPC; ++k) {
-      const int gi = (cb + k) / cpg;
-      const float2 q = mr[(int64_t)b * groups + gi];
-      const float2 cf = coef[(int64_t)b * groups + gi];
-      const float xh = (to_f(ex[k]) - q.x) * q.y;
-      const float gm = gamma[cb + k];
-      float dz = to_f(ed[k]);
-      if (act == LDM_ACT_SILU) dz *= silu_grad(xh * gm + beta[cb + k]);
-      r[k] = from_f<T>(q.y * gm * dz + cf.x + cf.y * xh + ad[k] + prev[k]);
+      for (int k = 0; k < EPC; k += 4) {
+        const float4 g4 = *reinterpret_cast<const float4*>(gamma + cb + k);
+        gm[k] = g4.x; gm[k + 1] = g4.y; gm[k + 2] = g4.z; gm[k + 3] = g4.w;
+        if (act == LDM_ACT_SILU) {
+          const float4 b4 = *reinterpret_cast<const float4*>(beta + cb + k);
+          bt[k] = b4.x; bt[k + 1] = b4.y; bt[k + 2] = b4.z; bt[k + 3] = b4.w;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) {
+        const bool hi = cb + k >= bnd;
+        const float qx = hi ? q1.x : q0.x, qy = hi ? q1.y : q0.y;
+        const float cx = hi ? f1.x : f0.x, cy = hi ? f1.y : f0.y;
+        const float xh = (to_f(ex[k]) - qx) * qy;
+        float dz = to_f(ed[k]);
+        if (act == LDM_ACT_SILU) dz *= silu_grad(xh * gm[k] + bt[k]);
+        r[k] = from_f<T>(qy * gm[k] * dz + cx + cy * xh + ad[k] + prev[k]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < EPC; ++k) {
+        const int gi = (cb + k) / cpg;
+        const float2 q = mr[(int64_t)b * groups + gi];
+        const float2 cf = coef[(int64_t)b * groups + gi];
+        const float xh = (to_f(ex[k]) - q.x) * q.y;
+        const float gm = gamma[cb + k];
+        float dz = to_f(ed[k]);
+        if (act == LDM_ACT_SILU) dz *= silu_grad(xh * gm + beta[cb + k]);
+        r[k] = from_f<T>(q.y * gm * dz + cf.x + cf.y * xh + ad[k] + prev[k]);
+      }
     }
     *reinterpret_cast<uint4*>(dst) = res;
   }
@@ -1033,6 +1101,7 @@ int wgrad_validate(const ldm_wgrad_params* q, int* es_out, int* M_out) {
   if ((int64_t)q->batch * q->h_out * q->w_out >= (1 << 24)) return LDM_ERR_ARG;   // reciprocal pixel decode
   const int cin = q->c0 + q->c1;
   if (q->kpad % 64 || q->ksize * q->ksize * cin > q->kpad || q->n <= 0) return LDM_ERR_ARG;
+  if ((int64_t)q->n * q->kpad >= (1LL << 31)) return LDM_ERR_ARG;   // 32-bit slab indexing
   if (q->cin_real <= 0 || q->cin_real > cin) return LDM_ERR_ARG;
   if (q->geglu && q->n % 32) return LDM_ERR_ARG;
   if (!aligned16(q->a0) || (q->a1 && !aligned16(q->a1)) || !aligned16(q->dy)) return LDM_ERR_ALIGN;
@@ -1050,10 +1119,11 @@ int wgrad_validate(const ldm_wgrad_params* q, int* es_out, int* M_out) {
 }  // namespace
 
 namespace {
-int g_wgrad_ring = 1;   // tuning / A-B hook (ldm_conv2d_wgrad_set_ring): 0 = two 64-pixel stages
+int g_wgrad_ring = 1;   // tuning / A-B hook (ldm_conv2d_wgrad_set_ring): 0 = two 64-pixel stages,
+                        // 2 = a five-slot ring (four stages in flight; stride-1 modes only)
 int g_wgrad_fast = 1;   // A-B hook (ldm_conv2d_wgrad_set_fast_loader): 0 = the general loader everywhere
 }  // namespace
-extern "C" void ldm_conv2d_wgrad_set_ring(int ring) { g_wgrad_ring = ring ? 1 : 0; }
+extern "C" void ldm_conv2d_wgrad_set_ring(int ring) { g_wgrad_ring = ring < 0 ? 0 : ring > 2 ? 2 : ring; }
 extern "C" void ldm_conv2d_wgrad_set_fast_loader(int on) { g_wgrad_fast = on ? 1 : 0; }
 
 extern "C" size_t ldm_conv2d_wgrad_workspace_bytes(const ldm_wgrad_params* q) {
@@ -1092,7 +1162,11 @@ extern "C" int ldm_conv2d_wgrad(const ldm_wgrad_params* q, ldm_stream_t stream) 
   const int mode = !g_wgrad_fast || !plain ? WG_GENERAL
                    : q->ksize == 1          ? WG_1X1
                    : 16 / q->w_out < q->h_out ? WG_PLAIN : WG_GENERAL;
-  if (q->dtype == LDM_BF16 && g_wgrad_ring && mode == WG_1X1)
+  if (q->dtype == LDM_BF16 && g_wgrad_ring == 2 && mode == WG_1X1)
+    hipLaunchKernelGGL((wgrad_kernel<bf16_t, 32, 5, WG_1X1>), dim3(blocks), dim3(256), 0, s, a);
+  else if (q->dtype == LDM_BF16 && g_wgrad_ring == 2 && mode == WG_PLAIN)
+    hipLaunchKernelGGL((wgrad_kernel<bf16_t, 32, 5, WG_PLAIN>), dim3(blocks), dim3(256), 0, s, a);
+  else if (q->dtype == LDM_BF16 && g_wgrad_ring && mode == WG_1X1)
     hipLaunchKernelGGL((wgrad_kernel<bf16_t, 32, 4, WG_1X1>), dim3(blocks), dim3(256), 0, s, a);
   else if (q->dtype == LDM_BF16 && g_wgrad_ring && mode == WG_PLAIN)
     hipLaunchKernelGGL((wgrad_kernel<bf16_t, 32, 4, WG_PLAIN>), dim3(blocks), dim3(256), 0, s, a);
@@ -1107,7 +1181,7 @@ extern "C" int ldm_conv2d_wgrad(const ldm_wgrad_params* q, ldm_stream_t stream) 
   return LDM_OK;
 }
 
-constexpr int COLSUM_RCHUNK = 256;
+constexpr int COLSUM_RCHUNK = 128;
 extern "C" size_t ldm_colsum_workspace_bytes(int rows, int c, int segments) {
   if (rows <= 0 || c <= 0 || segments <= 0) return 0;
   const int rps = rows / segments;

@@ -616,7 +616,7 @@ def set_attention_fp8_scaled(enabled=True):
 
 def set_wgrad_ring(ring=True):
     """Tuning / A-B hook: bf16 weight gradient on four 32-pixel LDS stages (default) or two 64-pixel."""
-    load_library().ldm_conv2d_wgrad_set_ring(int(bool(ring)))
+    load_library().ldm_conv2d_wgrad_set_ring(int(ring))
 
 
 def set_wgrad_fast_loader(enabled=True):
