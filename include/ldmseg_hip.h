@@ -469,6 +469,9 @@ void ldm_conv2d_wgrad_set_ring(int ring);
 /* A-B hook: 1 (default) = stride-1 weight gradients load their operands by per-lane pointers
  * advanced 16 rows per DMA (branch-free); 0 = the general pixel-decoding loader everywhere. */
 void ldm_conv2d_wgrad_set_fast_loader(int on);
+/* A-B hook: 1 (default) = 3x3 slab sums by wave-owned [64 channel][9 tap] blocks written as
+ * contiguous runs; 0 = one packed element per thread (stores 36 bytes apart). */
+void ldm_conv2d_wgrad_set_reduce3(int on);
 
 /* ldm_colsum — out[s][c] (+)= sum over the rows of segment s of x[rows][c] (segments split the
  * rows evenly).  Bias gradients (1 segment) and per-batch time-embedding gradients (batch

@@ -65,7 +65,7 @@ def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scal
     return run, 4.0 * B * heads * N * N * (C // heads), None
 
 
-def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False, ring=True, fast=True):
+def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False, ring=True, fast=True, r3=True):
     g = torch.Generator(device=DEV).manual_seed(0)
     x = torch.randn(B, H, W, Cin, device=DEV, generator=g).to(BF)
     dy = torch.randn(B, H, W, Cout, device=DEV, generator=g).to(BF)
@@ -76,6 +76,7 @@ def wgrad_case(B, H, W, Cin, Cout, k=3, geglu=False, ring=True, fast=True):
     def run():
         K.set_wgrad_ring(ring)
         K.set_wgrad_fast_loader(fast)
+        K.set_wgrad_reduce3(r3)
         return K.conv2d_wgrad(pc, x, B, H, W, dy, dw=dw)
     return run, 2.0 * B * H * W * Cout * k * k * Cin, None
 
@@ -334,6 +335,10 @@ CASES = {
     "wgrad_up_960_ns5": lambda: wgrad_case(16, 64, 64, 960, 320, ring=2),
     "wgrad_geglu_320_ns5": lambda: wgrad_case(16, 64, 64, 320, 2560, k=1, geglu=True, ring=2),
     "wgrad_qkv_320_ns5": lambda: wgrad_case(16, 64, 64, 320, 960, k=1, ring=2),
+    "wgrad_l0_320_r1": lambda: wgrad_case(16, 64, 64, 320, 320, r3=False),
+    "wgrad_l2_1280_r1": lambda: wgrad_case(16, 16, 16, 1280, 1280, r3=False),
+    "wgrad_l3_1280_r1": lambda: wgrad_case(16, 8, 8, 1280, 1280, r3=False),
+    "wgrad_up_960_r1": lambda: wgrad_case(16, 64, 64, 960, 320, r3=False),
     "wgrad_l0_320_old": lambda: wgrad_case(16, 64, 64, 320, 320, ring=False),
     "wgrad_l1_640_old": lambda: wgrad_case(16, 32, 32, 640, 640, ring=False),
     "wgrad_l2_1280_old": lambda: wgrad_case(16, 16, 16, 1280, 1280, ring=False),

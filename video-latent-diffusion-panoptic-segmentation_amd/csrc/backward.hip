@@ -327,6 +327,57 @@ __device__ __forceinline__ int geglu_packed_row(int nt, int half) {
   return (i >> 4) * 32 + 16 * hi + (i & 15);
 }
 
+// 3x3 form: the torch layout puts a channel's 9 taps together, so the element-per-thread form's
+// stores land 36 bytes apart.  Here a wave owns one packed row and 64 channels: lane c sums its 9
+// taps over the splits (9 coalesced 256-byte reads per split, splits in order as above), the wave
+// stages the [64 c][9 taps] block in LDS and writes it back as 9 contiguous 256-byte runs.
+__global__ __launch_bounds__(256) void wgrad_reduce3(const float* __restrict__ part, int splits, int n, int kpad,
+                                                     int cin_pad, int cin_real, int geglu, float* __restrict__ dst,
+                                                     int accumulate) {
+  __shared__ float st[4][64 * 9];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ncb = (cin_real + 63) / 64;
+  const int item = blockIdx.x * 4 + w;
+  if (item >= n * ncb) return;   // wave-uniform; no block barrier below
+  const int np = item / ncb, c0 = (item - np * ncb) * 64;
+  const int c = c0 + lane;
+  const int total = n * kpad;
+  float sum[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) sum[t] = 0.f;
+  if (c < cin_real) {
+    const float* src = part + (int64_t)np * kpad + c;
+    for (int sp = 0; sp < splits; ++sp) {
+      float v[9];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) v[t] = src[(int64_t)sp * total + t * cin_pad];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) sum[t] += v[t];
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t) st[w][lane * 9 + t] = sum[t];
+  // the wave's own LDS rows: a wavefront-scope fence orders the stores before the transposed reads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  int nt = np;
+  if (geglu) {  // inverse of geglu_packed_row
+    const int blk = np >> 5, r = np & 31, half = n >> 1;
+    nt = (r < 16) ? blk * 16 + r : half + blk * 16 + (r - 16);
+  }
+  const int nc = min(64, cin_real - c0);
+  float* out = dst + ((int64_t)nt * cin_real + c0) * 9;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    const int o = j * 64 + lane;
+    if (o < nc * 9) {
+      const float v = st[w][o];
+      out[o] = accumulate ? out[o] + v : v;
+    }
+  }
+}
+
 // Sum the split slab into the torch weight layout.  Thread per packed element (coalesced slab
 // reads).  dst[nt][c][ky][kx] (ksize 3) or dst[nt][c] (ksize 1), c < cin_real.
 __global__ __launch_bounds__(256) void wgrad_reduce(const float* __restrict__ part, int splits, int n, int kpad,
@@ -1121,10 +1172,12 @@ int wgrad_validate(const ldm_wgrad_params* q, int* es_out, int* M_out) {
 namespace {
 int g_wgrad_ring = 1;   // tuning / A-B hook (ldm_conv2d_wgrad_set_ring): 0 = two 64-pixel stages,
                         // 2 = a five-slot ring (four stages in flight; stride-1 modes only)
+int g_wgrad_reduce3 = 1;   // A-B hook (ldm_conv2d_wgrad_set_reduce3): 0 = element-per-thread 3x3 slab sum
 int g_wgrad_fast = 1;   // A-B hook (ldm_conv2d_wgrad_set_fast_loader): 0 = the general loader everywhere
 }  // namespace
 extern "C" void ldm_conv2d_wgrad_set_ring(int ring) { g_wgrad_ring = ring < 0 ? 0 : ring > 2 ? 2 : ring; }
 extern "C" void ldm_conv2d_wgrad_set_fast_loader(int on) { g_wgrad_fast = on ? 1 : 0; }
+extern "C" void ldm_conv2d_wgrad_set_reduce3(int on) { g_wgrad_reduce3 = on ? 1 : 0; }
 
 extern "C" size_t ldm_conv2d_wgrad_workspace_bytes(const ldm_wgrad_params* q) {
   int es = 0, M = 0;
@@ -1175,8 +1228,14 @@ extern "C" int ldm_conv2d_wgrad(const ldm_wgrad_params* q, ldm_stream_t stream) 
   else hipLaunchKernelGGL((wgrad_kernel<float, 64, 2>), dim3(blocks), dim3(256), 0, s, a);
   LDM_CHECK_LAUNCH();
   const int64_t total = (int64_t)q->n * q->kpad;
-  hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a.part, sp, q->n, q->kpad,
-                     q->ksize, a.cin, q->cin_real, q->geglu, q->dw, q->accumulate);
+  if (q->ksize == 3 && g_wgrad_reduce3) {
+    const int items = q->n * ((q->cin_real + 63) / 64);
+    hipLaunchKernelGGL(wgrad_reduce3, dim3((unsigned)((items + 3) / 4)), dim3(256), 0, s, a.part, sp, q->n, q->kpad,
+                       a.cin, q->cin_real, q->geglu, q->dw, q->accumulate);
+  } else {
+    hipLaunchKernelGGL(wgrad_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a.part, sp, q->n,
+                       q->kpad, q->ksize, a.cin, q->cin_real, q->geglu, q->dw, q->accumulate);
+  }
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }

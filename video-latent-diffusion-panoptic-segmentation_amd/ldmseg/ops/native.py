@@ -104,6 +104,7 @@ EXPORTS = {
     "ldm_attention_set_bwd32": (None, [_i]),
     "ldm_conv2d_wgrad_set_ring": (None, [_i]),
     "ldm_conv2d_wgrad_set_fast_loader": (None, [_i]),
+    "ldm_conv2d_wgrad_set_reduce3": (None, [_i]),
     "ldm_attention_set_waves": (None, [_i]),
     "ldm_attention_bwd_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_bwd": (_i, [ctypes.POINTER(AttnParams), _vp, _vp, _i, _vp, _vp, _vp, _vp, _i, _i, _vp, _vp]),
@@ -617,6 +618,12 @@ def set_attention_fp8_scaled(enabled=True):
 def set_wgrad_ring(ring=True):
     """Tuning / A-B hook: bf16 weight gradient on four 32-pixel LDS stages (default) or two 64-pixel."""
     load_library().ldm_conv2d_wgrad_set_ring(int(ring))
+
+
+def set_wgrad_reduce3(enabled=True):
+    """A-B hook: the 3x3 weight gradient's slab sum by wave-owned channel x tap blocks (default) or
+    one packed element per thread."""
+    load_library().ldm_conv2d_wgrad_set_reduce3(int(bool(enabled)))
 
 
 def set_wgrad_fast_loader(enabled=True):
