@@ -129,6 +129,8 @@ def test_train_step_keeps_inference_ln_fold():
     assert u.ln_fold
     ts = LDMTrainStep(u, DDIMNoiseScheduler())
     assert not u.ln_fold
+    u.train()
     with ts.for_inference() as m:
         assert m is u and u.ln_fold
-    assert not u.ln_fold
+        assert not u.training and u.upsample_phases        # eval mode inside: the phase form runs
+    assert not u.ln_fold and u.training

@@ -32,7 +32,10 @@ def test_phase_pack_reproduces_upsample_conv():
 
 
 def test_phase_pack_needs_upsample_flag():
+    """The upsample check comes before any device check: a phase pack called without
+    upsample=True is rejected with ValueError on any tensor (a CPU tensor used to
+    satisfy the test through the device check alone)."""
     pc = K.PackedConv(torch.randn(8, 8, 3, 3), None, torch.float32, upsample_phases=True)
     import pytest
-    with pytest.raises((ValueError, RuntimeError)):
-        K.conv2d(pc, torch.empty(1, 4, 4, 8), 1, 4, 4)                       # CPU tensor / no upsample
+    with pytest.raises(ValueError, match="upsample_phases"):
+        K.conv2d(pc, torch.empty(1, 4, 4, 8), 1, 4, 4)

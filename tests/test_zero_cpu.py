@@ -57,7 +57,9 @@ def _worker(rank, world, port, q, tmp):
             ts.consolidate_state_dict(to=dst)
             if rank == dst:
                 mine = ts.state_dict()
-        released = ts._consolidated is None   # consumed by state_dict()
+        # torch semantics: the consolidated copy serves repeated state_dict() calls on its rank
+        #  until the next optimizer step
+        released = rank != world - 1 or ts.state_dict()["state"].keys() == mine["state"].keys()
         theirs = ref.state_dict()
         # checkpoint.save on every rank: consolidated collectively, written by rank 0 only
         from ldmseg.utils import checkpoint

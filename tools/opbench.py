@@ -249,6 +249,9 @@ CASES = {
     "gemm_short_l2_2560": lambda: conv_case(8, 16, 16, 2560, 1280, k=1, c1=1280, residual=True),
     "gemm_short_l2_1920": lambda: conv_case(8, 16, 16, 1920, 1280, k=1, c1=640, residual=True),
     "gemm_qkv_1280": lambda: conv_case(8, 16, 16, 1280, 3840, k=1),
+    "gemm_qkv_1280_l3": lambda: conv_case(8, 8, 8, 1280, 3840, k=1),
+    "gemm_geglu_1280_l3": lambda: conv_case(8, 8, 8, 1280, 10240, k=1, geglu=True),
+    "gemm_ff2_5120_l3": lambda: conv_case(8, 8, 8, 5120, 1280, k=1, residual=True),
     "gemm_ff2_5120": lambda: conv_case(8, 16, 16, 5120, 1280, k=1, residual=True),
     "gemm_geglu_1280_l2": lambda: conv_case(8, 16, 16, 1280, 10240, k=1, geglu=True),
     "conv3_l3_2560": lambda: conv_case(8, 8, 8, 2560, 1280, c1=1280, residual=True, stats=True),
@@ -278,6 +281,11 @@ CASES = {
     "mm_ff2_2560": lambda: mm_case(8192, 2560, 640),
     "mm_geglu_1280": lambda: mm_case(2048, 1280, 10240),
     "mm_proj_1280": lambda: mm_case(2048, 1280, 1280),
+    "mm_qkv_1280": lambda: mm_case(2048, 1280, 3840),
+    "mm_ff2_5120": lambda: mm_case(2048, 5120, 1280),
+    "mm_proj_1280_l3": lambda: mm_case(512, 1280, 1280),
+    "mm_qkv_1280_l3": lambda: mm_case(512, 1280, 3840),
+    "mm_geglu_1280_l3": lambda: mm_case(512, 1280, 10240),
     "mm_conv_l0_320": lambda: mm_case(32768, 2880, 320),
     "mm_conv_l1_640": lambda: mm_case(8192, 5760, 640),
     "mm_conv_l2_1280": lambda: mm_case(2048, 11520, 1280),

@@ -452,6 +452,8 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
     row_stats: a zeroed fp64 [M, 2] tensor the epilogue adds each output row's (sum, sumsq) to.
     ln = (rows, eps): x0's rows are LayerNorm'd inside the GEMM (pc from packed_ln_fold, rows =
     the producer's row_stats)."""
+    if getattr(pc, "phases", False) and not upsample:
+        raise ValueError("an upsample_phases pack is the nearest-2x upsample conv: pass upsample=True")
     lib = load_library()
     _gpu(x0, x1, pc.w, temb, residual, out)
     c0 = x0.numel() // (batch * h * w)
@@ -465,8 +467,6 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
     if x0.dtype != pc.dtype or (x1 is not None and x1.dtype != pc.dtype):
         raise TypeError(f"conv input dtype {x0.dtype} != packed weight dtype {pc.dtype}")
     if getattr(pc, "phases", False):
-        if not upsample:
-            raise ValueError("an upsample_phases pack is the nearest-2x upsample conv: pass upsample=True")
         if (h * w) % 32 or x1 is not None or stride != 1 or pad_mode or out_layout != OUT_NHWC or \
                 row_stats is not None or ln is not None:
             pc = pc.gather                 # shapes the phase form does not take: the 3x3 gather form

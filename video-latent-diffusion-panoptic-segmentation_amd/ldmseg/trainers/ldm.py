@@ -233,7 +233,9 @@ class LDMTrainStep:
         of the group must call it); gathers the sharded AdamW moments.  Only rank ``to`` (a rank of
         the group) keeps them, in host memory, so that state_dict() can then be called there alone
         (rank 0 inside checkpoint.save); the other ranks keep nothing, and the GPU temporaries of
-        the gather are released before this returns.  No-op without ZeRO."""
+        the gather are released before this returns.  The host copy stays valid (state_dict() may be
+        called on it any number of times, as with torch's ZeroRedundancyOptimizer) until the next
+        optimizer step.  No-op without ZeRO."""
         if not self.zero:
             return
         keep = self.rank == to
@@ -249,14 +251,13 @@ class LDMTrainStep:
         (never a collective).  Under ZeRO it needs consolidate_state_dict(to=this rank) on every
         rank first, as torch's ZeroRedundancyOptimizer does, and raises otherwise — a rank-0-only
         save can then never block inside a collective the other ranks do not join.  The
-        consolidated host copy is consumed: it is released once the state dict is built."""
+        consolidated host copy serves every call until the next step() releases it."""
         if self.zero:
             c = self._consolidated
             if c is None or c[0] != self.step_count:
                 raise RuntimeError("ZeRO optimizer state is sharded: call consolidate_state_dict(to=rank) on every "
                                    "rank (checkpoint.save does) before state_dict() on that rank")
             exp_avg, exp_avg_sq = c[1], c[2]
-            self._consolidated = None
         else:
             exp_avg, exp_avg_sq = self.exp_avg, self.exp_avg_sq
         state, pgs, idx = {}, [], 0
@@ -334,12 +335,16 @@ class LDMTrainStep:
                 latents = sample_latents(unet, ...)
 
         The packs are rebuilt for the folded plan on entry and for the training plan on exit
-        (one prepare() each way)."""
+        (one prepare() each way).  The module is put in eval mode inside the context (the
+        phase-form upsample conv runs only in eval mode) and its previous mode is restored on exit."""
+        was_training = self.unet.training
         self.unet.set_ln_fold(self._inference_fold)
         self.unet.set_upsample_phases(self._inference_phases)
+        self.unet.eval()
         try:
             yield self.unet
         finally:
+            self.unet.train(was_training)
             self.unet.set_ln_fold(False)
             self.unet.set_upsample_phases(False)
 
@@ -388,6 +393,7 @@ class LDMTrainStep:
         """clip_grad_norm_ + AdamW step over the (reduced) flat gradient: this rank's shard under
         ZeRO, followed by the parameter all-gather."""
         self.step_count += 1
+        self._consolidated = None                           # the consolidated moments are now stale
         K.sq_norm(self.flat.grad, out=self.sqsum)          # the whole reduced gradient (clip_grad_norm_)
         lo, hi = self.shard
         if self.nseg:

@@ -61,9 +61,20 @@ def save(path, **kw):
     builds and writes the dict."""
     import torch.distributed as dist
     opt = kw.get("opt")
+    dist_on = dist.is_available() and dist.is_initialized()
+    writer = 0                              # global rank that builds and writes the dict
     if hasattr(opt, "consolidate_state_dict"):
-        opt.consolidate_state_dict()
-    if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
+        # consolidate onto the writer: `to` is a rank of the optimizer's own process group, so map
+        # global rank 0 into it; a group without global rank 0 consolidates to (and is written by)
+        # its own first rank
+        to, group = 0, getattr(opt, "group", None)
+        if dist_on and group is not None:
+            try:
+                to = dist.get_group_rank(group, 0)
+            except (ValueError, RuntimeError):
+                writer = dist.get_global_rank(group, 0)
+        opt.consolidate_state_dict(to=to)
+    if dist_on and dist.get_rank() != writer:
         return
     torch.save(construct_save_dict(**kw), str(path))
 
