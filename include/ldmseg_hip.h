@@ -144,6 +144,9 @@ void ldm_conv2d_set_ars(int mode);
  * 0 = planner's choice (>= 256 tiles), 1 = never, 2 = whenever legal (256-row tiles),
  * 3 = whenever legal with 128-row tiles. */
 void ldm_conv2d_set_wide(int mode);
+/* Tuning hook: the deep-ring 1x1 GEMM of the 16x16 / 8x8 levels (csrc/gemm_ring.hip): 0 planner, 1 never,
+   2 whenever legal. */
+void ldm_conv2d_set_ring(int mode);
 /* Tuning hook: column width of the split-K reduction kernel's 64-row tiles — 0 = planner's choice
  * (64 when 128-wide tiles give fewer than 512 blocks), 64 or 128 forced. */
 void ldm_conv2d_set_splitk_cols(int cols);
@@ -291,6 +294,18 @@ int ldm_group_norm_ex(const void* x0, const void* x1, int c0, int c1, int batch,
  * ------------------------------------------------------------------------------------- */
 int ldm_layer_norm(const void* x, int rows, int c, const float* gamma, const float* beta,
                    float eps, int act, void* out, int dtype, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * ldm_linear_rows — out[m][:] = act(x[m] . W^T + bias) for rows <= 16 (the time-embedding MLP:
+ * diffusers TimestepEmbedding linear_1 / linear_2 and the batched ResnetBlock2D time_emb_proj,
+ * unet.py:301-307 and every resnet's temb input).  x bf16 [rows][k]; x == NULL takes the row
+ * as the sinusoidal projection of t (the ldm_timestep_proj values rounded to bf16, dim = k).
+ * W packed bf16 [n][kpad] (n % 16 == 0, k % 32 == 0, k <= 1536), bias fp32 [n] or NULL,
+ * out [rows][n] fp32 or bf16 (16-byte aligned).
+ * ------------------------------------------------------------------------------------- */
+int ldm_linear_rows(const void* x, const float* t, int n_t, const float* freqs, int flip_sin_to_cos,
+                    const void* w, int kpad, int k, int n, const float* bias, int rows, int act, void* out,
+                    int out_dtype, ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * ldm_timestep_proj — sinusoidal timestep projection (diffusers Timesteps, unet.py:305):

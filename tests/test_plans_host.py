@@ -62,8 +62,24 @@ def test_single_frame_convs_fill_the_chip(hw, c0, c1, n):
 
 @pytest.mark.parametrize("M,kin,n", [(1024, 2560, 640), (256, 5120, 1280), (64, 5120, 1280)])
 def test_single_frame_deep_gemms_split(M, kin, n):
+    """Few rows, deep K: split K over >= 128 blocks, or one deep-ring tile per CU (no split)."""
     pl = _p(batch=M, h=1, w=1, c0=kin, n=n, ksize=1, residual=True)
-    assert pl["ksplit"] > 1 and pl["blocks"] >= 128, pl
+    assert (pl["ksplit"] > 1 or pl["kind"] == "ring") and pl["blocks"] >= 128, pl
+
+
+def test_deep_level_gemms_on_the_ring():
+    """The 16x16 / 8x8 levels' 1x1 GEMMs at B = 8 (proj_in / to_out / proj_out, the
+    16x16 up-block shortcuts) run on the deep-ring kernel, one tile per CU."""
+    for M, c0, c1, n, kw in ((2048, 1280, 0, 1280, dict(residual=True, gn_stats=True)),
+                             (2048, 1280, 0, 1280, dict(row_stats=True)),
+                             (2048, 1280, 1280, 1280, {}), (2048, 1280, 640, 1280, {}),
+                             (512, 1280, 0, 1280, dict(residual=True, gn_stats=True))):
+        pl = _p(batch=M // 64 if kw.get("gn_stats") else M, h=8 if kw.get("gn_stats") else 1,
+                w=8 if kw.get("gn_stats") else 1, c0=c0, c1=c1, n=n, ksize=1, **kw)
+        assert pl["kind"] == "ring" and pl["blocks"] == 256, (M, c0, c1, n, kw, pl)
+    # ff.net.2 (K = 5120) and the 8x8 concat shortcut keep their split-K tiles
+    for M, c0, c1 in ((2048, 5120, 0), (512, 5120, 0), (512, 1280, 1280)):
+        assert _p(batch=M, h=1, w=1, c0=c0, c1=c1, n=1280, ksize=1, residual=True)["kind"] == "tile"
 
 
 def test_describe_plan_rejects_what_conv2d_rejects():

@@ -383,8 +383,13 @@ def main():
                     help="short-K 1x1 GEMM modes to compare (ldm_conv2d_set_ars: 0 planner, 1 never, 2 when legal)")
     ap.add_argument("--wide", nargs="*", type=int, default=[0],
                     help="wide-tile persistent 1x1 GEMM modes (ldm_conv2d_set_wide: 0 planner, 1 never, 2 BM 256, 3 BM 128)")
+    ap.add_argument("--ring", nargs="*", type=int, default=[0],
+                    help="deep-ring 1x1 GEMM modes to compare (ldm_conv2d_set_ring: 0 planner, 1 never, 2 when legal)")
     ap.add_argument("--skcols", nargs="*", type=int, default=[0],
                     help="split-K reduction tile widths to compare (ldm_conv2d_set_splitk_cols: 0 planner, 64, 128)")
+    ap.add_argument("--graph", action="store_true",
+                    help="time each case as a captured HIP graph of --iters launches (device time: the eager loop "
+                         "is host-bound below ~20 us per launch)")
     ap.add_argument("--batch", type=int, default=8, help="B of the conv / GEMM cases (config 2: 1)")
     a = ap.parse_args()
     global BATCH
@@ -400,34 +405,53 @@ def main():
             continue
         for pl in a.plans:
             for gm in a.groups:
-                for am, sk, wd in [(x, y, z) for x in a.ars for y in a.skcols for z in a.wide]:
+                for am, sk, wd, rg in [(x, y, z, r) for x in a.ars for y in a.skcols for z in a.wide for r in a.ring]:
                     run, fl, nb = CASES[n]()
                     f = [0, 0, 1, 0] if pl == "auto" else [int(v) for v in pl.split(",")] + [0]
                     bm, bn, ks, st = f[:4]
 
-                    def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm, am=am, sk=sk, wd=wd):
+                    def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm, am=am, sk=sk, wd=wd, rg=rg):
                         K.set_conv_splitk_cols(sk)
                         K.force_conv_plan(bm, bn, ks)
                         K.force_conv_stages(st)
                         K.set_conv_raster_group(gm)
                         K.set_conv_ars(am)
                         K.set_conv_wide(wd)
+                        K.set_conv_ring(rg)
                         return run()
                     name = n if pl == "auto" else f"{n}@{pl}"
                     name = name if len(a.groups) == 1 else f"{name}/g{gm}"
                     name = name if len(a.ars) == 1 else f"{name}/ars{am}"
                     name = name if len(a.skcols) == 1 else f"{name}/skc{sk}"
-                    built[name if len(a.wide) == 1 else f"{name}/w{wd}"] = (run_pl, fl, nb)
+                    name = name if len(a.wide) == 1 else f"{name}/w{wd}"
+                    built[name if len(a.ring) == 1 else f"{name}/ring{rg}"] = (run_pl, fl, nb)
     for n, (run, _, _) in built.items():
         run()
     torch.cuda.synchronize()
+    graphs = {}
+    if a.graph:
+        for n, (run, _, _) in built.items():
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                run()
+            torch.cuda.current_stream().wait_stream(side)
+            gr = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gr):
+                for _ in range(a.iters):
+                    run()
+            graphs[n] = gr
+        torch.cuda.synchronize()
     res = {n: [] for n in built}
     for rnd in range(3):
         for n, (run, _, _) in built.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            for _ in range(a.iters):
-                run()
+            if a.graph:
+                graphs[n].replay()
+            else:
+                for _ in range(a.iters):
+                    run()
             e1.record()
             torch.cuda.synchronize()
             res[n].append(e0.elapsed_time(e1) / a.iters)

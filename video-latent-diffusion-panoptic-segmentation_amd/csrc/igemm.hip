@@ -27,6 +27,9 @@
 namespace ldm_igemm {   // gemm_wide.hip
 int wide_bm(const ldm_conv_params* q, int es, bool mixed, int M, bool plan_forced);
 int launch_wide(ConvArgs a, hipStream_t s, int bm);
+int ring_cfg(const ldm_conv_params* q, int es, bool mixed, int M, bool plan_forced, RingCfg* out);   // gemm_ring.hip
+int launch_ring(ConvArgs a, hipStream_t s, const RingCfg& c);
+int ring_abl();
 }  // namespace ldm_igemm
 
 namespace {
@@ -1401,7 +1404,9 @@ extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   const bool mixed = is_mixed(q, es);
   const int hks = halo_plan(q, es, mixed);
   if (hks) return hks > 1 ? (size_t)hks * M * q->n * sizeof(float) : 0;
-  if (ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0) || use_ars(q, es, mixed, M)) return 0;
+  if (ldm_igemm::ring_cfg(q, es, mixed, M, g_force_bm != 0, nullptr) ||
+      ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0) || use_ars(q, es, mixed, M))
+    return 0;
   const Plan pl = make_plan(q, M, es, mixed);
   return pl.ksplit > 1 ? (size_t)pl.ksplit * M * q->n * sizeof(float) : 0;
 }
@@ -1415,6 +1420,11 @@ extern "C" int ldm_conv2d_describe_plan(const ldm_conv_params* q, int* out) {
   const bool mixed = is_mixed(q, es);
   const int hks = halo_plan(q, es, mixed);
   const bool halo = hks > 0;
+  ldm_igemm::RingCfg rc{0, 0, 0};
+  if (!halo && ldm_igemm::ring_cfg(q, es, mixed, M, g_force_bm != 0, &rc)) {
+    out[0] = 5; out[1] = rc.bm; out[2] = rc.bn; out[3] = 1; out[4] = 0;
+    return LDM_OK;
+  }
   const int wbm = halo ? 0 : ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0);
   const bool ars = !halo && !wbm && use_ars(q, es, mixed, M);
   if (halo || wbm || ars) {
@@ -1444,9 +1454,11 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   const bool mixed = is_mixed(q, es);
   const int hks = halo_plan(q, es, mixed);
   const bool use_halo = hks > 0;
-  const int wbm = use_halo ? 0 : ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0);
-  const bool ars = !use_halo && !wbm && use_ars(q, es, mixed, M);
-  const Plan pl = use_halo ? Plan{0, 0, hks} : ((wbm || ars) ? Plan{0, 0, 1} : make_plan(q, M, es, mixed));
+  ldm_igemm::RingCfg rc{0, 0, 0};
+  const bool ring = !use_halo && ldm_igemm::ring_cfg(q, es, mixed, M, g_force_bm != 0, &rc) != 0;
+  const int wbm = (use_halo || ring) ? 0 : ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0);
+  const bool ars = !use_halo && !ring && !wbm && use_ars(q, es, mixed, M);
+  const Plan pl = use_halo ? Plan{0, 0, hks} : ((ring || wbm || ars) ? Plan{0, 0, 1} : make_plan(q, M, es, mixed));
   if (pl.ksplit > 1) {
     const size_t need = (size_t)pl.ksplit * M * q->n * sizeof(float);
     if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;
@@ -1489,6 +1501,10 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.ln_eps = q->ln_eps;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (use_halo) return launch_halo(a, s);
+  if (ring) {
+    a.abl = ldm_igemm::ring_abl();
+    return ldm_igemm::launch_ring(a, s, rc);
+  }
   if (wbm) return ldm_igemm::launch_wide(a, s, wbm);
   if (ars) return launch_ars(a, s);
   if (pl.bm == 256) return launch_big(a, s);

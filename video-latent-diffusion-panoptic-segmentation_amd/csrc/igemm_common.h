@@ -38,7 +38,10 @@ struct ConvArgs {
   int group_m;        // M panels per raster group (grouped_tile); 1 = plain row-major tiles
   int phase;          // nearest-2x upsample + 3x3 conv as four 2x2 phase convs (ldm_conv2d upsample 3):
                       // rows m = (b, phase, y, x) over the low-res grid, W = [4][n][kpad]
+  int abl;            // ablation mode of the deep-ring GEMM (tuning hook; 0 = normal)
 };
+// deep-ring 1x1 GEMM configuration (gemm_ring.hip): id 0 = not the ring kernel
+struct RingCfg { int id, bm, bn; };
 // Storage row of GEMM row m: m itself, or in phase mode (rows ordered (b, phase (dy, dx), y, x) over
 // the h_in x w_in input grid) the output pixel (b, 2y + dy, 2x + dx) of the 2x upsampled image —
 // batch-major either way, so m / hw_out is the batch in both.

@@ -45,6 +45,84 @@ __global__ void tproj_kernel(const float* __restrict__ t, int n_t, int batch, co
   }
 }
 
+
+// ------------------------------------------------------------------ few-row linear (time embedding)
+// out[m][n] = act(x[m] . W[n] + bias[n]) for rows <= 16: the time-embedding MLP (diffusers
+// TimestepEmbedding linear_1 / linear_2, unet.py:305-307) and the batched time_emb_proj of every
+// ResNet — GEMV-shaped (B = 8 rows), bound by streaming the packed weight once.  One 16-column group
+// per block; the block's four waves split K into k32 steps and issue every weight / input load of
+// their share before the first MFMA (v_mfma_f32_16x16x32_bf16, rows padded to 16); the four partial
+// tiles are summed in a fixed order through LDS.  x == NULL: the input row is the sinusoidal timestep
+// projection (diffusers Timesteps, the tproj_kernel values rounded to bf16) computed in place.
+constexpr int LR_MAXS = 12;   // k32 steps per wave held in registers (K <= 4 * 32 * 12 = 1536)
+
+__global__ __launch_bounds__(256) void linear_rows_kernel(const bf16_t* __restrict__ x, const float* __restrict__ t,
+                                                          int n_t, const float* __restrict__ freqs, int flip,
+                                                          const bf16_t* __restrict__ w, int kpad, int k, int n,
+                                                          const float* __restrict__ bias, int rows, int act, void* out,
+                                                          int out_dt) {
+  __shared__ f32x4_t part[3][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lr = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * 16;
+  const int nk = k / 32;
+  const int s0 = nk * wave / 4, s1 = nk * (wave + 1) / 4;
+  uint4 wb[LR_MAXS], xa[LR_MAXS];
+  const bf16_t* wrow = w + (int64_t)(n0 + lr) * kpad + 8 * g;
+#pragma unroll
+  for (int i = 0; i < LR_MAXS; ++i)
+    if (s0 + i < s1) wb[i] = *reinterpret_cast<const uint4*>(wrow + (s0 + i) * 32);
+  if (x) {
+#pragma unroll
+    for (int i = 0; i < LR_MAXS; ++i)
+      if (s0 + i < s1)
+        xa[i] = lr < rows ? *reinterpret_cast<const uint4*>(x + (int64_t)lr * k + (s0 + i) * 32 + 8 * g)
+                          : make_uint4(0u, 0u, 0u, 0u);
+  } else {
+    const int half = k / 2;
+    const float tv = lr < rows ? t[n_t == 1 ? 0 : lr] : 0.f;
+#pragma unroll
+    for (int i = 0; i < LR_MAXS; ++i) {
+      if (s0 + i >= s1) continue;
+      bf16_t h[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int j = (s0 + i) * 32 + 8 * g + e;
+        const bool first = j < half;
+        const float arg = tv * freqs[first ? j : j - half];
+        const bool use_cos = flip ? first : !first;          // [sin || cos], flipped to [cos || sin]
+        h[e] = lr < rows ? f2bf(use_cos ? cosf(arg) : sinf(arg)) : (bf16_t)0;
+      }
+      xa[i] = *reinterpret_cast<const uint4*>(h);
+    }
+  }
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < LR_MAXS; ++i) {
+    if (s0 + i >= s1) continue;
+    Frag8<bf16_t> a, b;
+    a.v = wb[i];
+    b.v = xa[i];
+    mma_k32(acc, a, b);                  // D[n][m]: lane (g, lr) holds columns 4g..4g+3 of row lr
+  }
+  if (wave > 0) part[wave - 1][lane] = acc;
+  __syncthreads();
+  if (wave > 0) return;
+#pragma unroll
+  for (int q = 0; q < 3; ++q) acc += part[q][lane];
+  if (lr >= rows) return;
+  const int nc = n0 + 4 * g;
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = act_f(acc[r] + (bias ? bias[nc + r] : 0.f), act);
+  if (out_dt == LDM_F32) {
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + (int64_t)lr * n + nc) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    bf16_t h[4] = {f2bf(v[0]), f2bf(v[1]), f2bf(v[2]), f2bf(v[3])};
+    *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(out) + (int64_t)lr * n + nc) = *reinterpret_cast<const uint2*>(h);
+  }
+}
+
 // ------------------------------------------------------------------ DDIM
 struct DdimArgs {
   const void* mo; int mo_dt;
@@ -199,6 +277,21 @@ extern "C" int ldm_timestep_proj(const float* t, int n_t, int batch, const float
   if (dtype != LDM_F32 && dtype != LDM_BF16) return LDM_ERR_ARG;
   hipLaunchKernelGGL(tproj_kernel, dim3(grid_for((int64_t)batch * dim)), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), t, n_t, batch, freqs, dim, flip, out, dtype);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
+}
+
+extern "C" int ldm_linear_rows(const void* x, const float* t, int n_t, const float* freqs, int flip, const void* w,
+                               int kpad, int k, int n, const float* bias, int rows, int act, void* out, int out_dtype,
+                               ldm_stream_t stream) {
+  if (!w || !out || rows <= 0 || rows > 16 || n <= 0 || n % 16 || k <= 0 || k % 32 || k > kpad || kpad % 8) return LDM_ERR_ARG;
+  if (k > 4 * 32 * LR_MAXS || (out_dtype != LDM_F32 && out_dtype != LDM_BF16)) return LDM_ERR_ARG;
+  if (act < LDM_ACT_NONE || act > LDM_ACT_SIGMOID) return LDM_ERR_ARG;
+  if (!x && (!t || !freqs || k % 2 || (n_t != 1 && n_t != rows))) return LDM_ERR_ARG;
+  if ((x && !aligned16(x)) || !aligned16(w) || !aligned16(out) || (reinterpret_cast<uintptr_t>(out) & 15)) return LDM_ERR_ALIGN;
+  hipLaunchKernelGGL(linear_rows_kernel, dim3(n / 16), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     reinterpret_cast<const bf16_t*>(x), t, n_t, freqs, flip, reinterpret_cast<const bf16_t*>(w), kpad,
+                     k, n, bias, rows, act, out, out_dtype);
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }

@@ -680,10 +680,19 @@ class UNet(nn.Module):
         if not torch.is_tensor(timestep):
             timestep = torch.tensor([timestep], device=dev)
         t = timestep.reshape(-1).to(device=dev, dtype=torch.float32)
-        emb = K.timestep_proj(t, B, P["freqs"], self.time_proj.num_channels, self.time_proj.flip_sin_to_cos, dt)
-        emb = K.linear(P["lin1"], emb, act=K.ACT_SILU)
-        emb = K.linear(P["lin2"], emb, act=K.ACT_SILU)                   # = SiLU(time_embedding(t))
-        temb_all = K.linear(P["temb_proj"], emb, out_dtype=torch.float32)  # [B, sum Cout]
+        if dt == torch.bfloat16 and P["lin1"].cin == self.time_proj.num_channels and all(
+                K.linear_rows_ok(P[k], B) for k in ("lin1", "lin2", "temb_proj")):
+            # few-row GEMMs that stream each weight once (ldm_linear_rows); the sinusoid is formed
+            # inside linear_1's launch
+            emb = K.linear_rows(P["lin1"], None, B, act=K.ACT_SILU, t=t, freqs=P["freqs"],
+                                flip_sin_to_cos=self.time_proj.flip_sin_to_cos)
+            emb = K.linear_rows(P["lin2"], emb, B, act=K.ACT_SILU)     # = SiLU(time_embedding(t))
+            temb_all = K.linear_rows(P["temb_proj"], emb, B, out_dtype=torch.float32)
+        else:
+            emb = K.timestep_proj(t, B, P["freqs"], self.time_proj.num_channels, self.time_proj.flip_sin_to_cos, dt)
+            emb = K.linear(P["lin1"], emb, act=K.ACT_SILU)
+            emb = K.linear(P["lin2"], emb, act=K.ACT_SILU)               # = SiLU(time_embedding(t))
+            temb_all = K.linear(P["temb_proj"], emb, out_dtype=torch.float32)  # [B, sum Cout]
         # 3. conv_in (unet.py:357)
         x = K.nchw_to_nhwc(sources, P["cin_pad"], dt)
         x = K.conv2d(P["conv_in"], x, B, H, W, gn_stats=True)

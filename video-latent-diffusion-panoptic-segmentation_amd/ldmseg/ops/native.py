@@ -75,6 +75,7 @@ EXPORTS = {
     "ldm_conv2d_set_halo_rows32": (None, [_i]),
     "ldm_conv2d_set_ars": (None, [_i]),
     "ldm_conv2d_set_wide": (None, [_i]),
+    "ldm_conv2d_set_ring": (None, [_i]),
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_feedforward": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
@@ -89,6 +90,7 @@ EXPORTS = {
     "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _i, _i, _vp, _i, _vp]),
     "ldm_layer_norm": (_i, [_vp, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp]),
     "ldm_timestep_proj": (_i, [_vp, _i, _i, _vp, _i, _i, _vp, _i, _vp]),
+    "ldm_linear_rows": (_i, [_vp, _vp, _i, _vp, _i, _vp, _i, _i, _i, _vp, _i, _i, _vp, _i, _vp]),
     "ldm_ddim_step": (_i, [ctypes.POINTER(DdimParams), _vp]),
     "ldm_ddim_add_noise": (_i, [_vp, _vp, _vp, _vp, _i, _f, _i, _i64, _vp, _i, _vp]),
     "ldm_ddim_remove_noise": (_i, [_vp, _vp, _vp, _vp, _i, _f, _i, _i64, _vp, _i, _vp]),
@@ -541,7 +543,7 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
     return out
 
 
-PLAN_KINDS = {0: "tile", 1: "halo", 2: "wide", 3: "ars", 4: "big"}
+PLAN_KINDS = {0: "tile", 1: "halo", 2: "wide", 3: "ars", 4: "big", 5: "ring"}
 
 
 def describe_plan(batch, h, w, c0, n, *, c1=0, ksize=3, stride=1, upsample=False, out_layout=OUT_NHWC,
@@ -691,6 +693,12 @@ def set_conv_wide(mode=0):
     """Tuning hook: wide-tile persistent 1x1 GEMM — 0 planner, 1 never, 2 whenever legal (256-row
     tiles), 3 whenever legal (128-row tiles)."""
     load_library().ldm_conv2d_set_wide(int(mode))
+
+
+def set_conv_ring(mode=0):
+    """Tuning hook: deep-ring 1x1 GEMM of the 16x16 / 8x8 levels — 0 planner, 1 never, 2 whenever
+    legal."""
+    load_library().ldm_conv2d_set_ring(int(mode))
 
 
 def set_conv_splitk_cols(cols=0):
@@ -973,6 +981,29 @@ def layer_norm(x, gamma, beta, eps, act=ACT_NONE, out=None):
     _check(lib.ldm_layer_norm(_ptr(x), rows, C, _ptr(gamma), _ptr(beta), float(eps), act, _ptr(out),
                               dtype_code(x.dtype), _stream(x)), "ldm_layer_norm")
     _prof_stop(ev, "layer_norm", 0.0, 2.0 * out.numel() * out.element_size())
+    return out
+
+
+def linear_rows_ok(pc: PackedConv, rows, x=None):
+    """ldm_linear_rows takes this bf16 linear over `rows` (<= 16) rows."""
+    k = pc.cin
+    return (pc.dtype == torch.bfloat16 and pc.ksize == 1 and 0 < rows <= 16 and pc.n % 16 == 0 and k % 32 == 0
+            and k <= 1536 and (x is None or (x.dtype == torch.bfloat16 and x.is_contiguous())))
+
+
+def linear_rows(pc: PackedConv, x, rows, *, act=ACT_NONE, out_dtype=None, t=None, freqs=None, flip_sin_to_cos=True):
+    """out [rows, n] = act(x @ W^T + b) for a handful of rows (ldm_linear_rows: the time-embedding
+    MLP); x=None with (t, freqs): the input row is the sinusoidal timestep projection of t."""
+    lib = load_library()
+    dev = pc.w.device
+    _gpu(pc.w, x, t, freqs)
+    if x is not None and x.numel() != rows * pc.cin:
+        raise ValueError("x must be [rows, cin]")
+    out_dtype = out_dtype or pc.dtype
+    out = torch.empty(rows, pc.n, dtype=out_dtype, device=dev)
+    _check(lib.ldm_linear_rows(_ptr(x), _ptr(t), 0 if t is None else t.numel(), _ptr(freqs), int(flip_sin_to_cos),
+                               _ptr(pc.w), pc.kpad, pc.cin, pc.n, _ptr(pc.bias), rows, act, _ptr(out),
+                               dtype_code(out_dtype), _stream(pc.w)), "ldm_linear_rows")
     return out
 
 
