@@ -296,6 +296,46 @@ int ldm_layer_norm(const void* x, int rows, int c, const float* gamma, const flo
                    float eps, int act, void* out, int dtype, ldm_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
+ * ldm_unet_tail — the UNet tail in one launch (unet.py:428-431): GroupNorm(conv_norm_out) ->
+ * SiLU -> conv_out (3x3, pad 1, c -> cout <= 4) -> NCHW model output, optionally followed by the
+ * sampler's DDIM step on it (ddim_scheduler.py:218-269; the ldm_ddim_step arithmetic).
+ * h: bf16 NHWC [batch][height][width][c] with its producer's GroupNorm accumulators (ldm_conv2d
+ * gn_partial: fp64 [batch][gn_slots][c / gn_unit][2]); height % 2 == 0, width % 16 == 0,
+ * width <= 64, c % 64 == 0, c <= 640, groups <= 64.  w: the conv_out weight packed as ldm_conv2d
+ * takes it (bf16 [cout][kpad], k = (ky, kx, c)).  eps_out (optional when the DDIM step is fused):
+ * NCHW [batch][cout][height][width] in eps_dtype; the model output is rounded to eps_dtype
+ * before the DDIM step, as the unfused path stores it.  prev / x0 (either may be NULL; both
+ * NULL: no DDIM step): NCHW in out_dtype; sample NCHW in sample_dtype.
+ * ------------------------------------------------------------------------------------- */
+typedef struct {
+  const void* h;
+  int batch, height, width, c;
+  const double* gn_acc;
+  int gn_unit, gn_slots, groups;
+  float eps;
+  const float* gamma;
+  const float* beta;
+  const void* w;
+  int kpad, cout;
+  const float* bias;
+  void* eps_out;
+  int eps_dtype;
+  const void* sample;
+  int sample_dtype;
+  const int64_t* t;                      /* device int64 [1] */
+  const float* alphas_cumprod;
+  float final_alpha_cumprod;
+  int step_ratio, prediction_type, clip_sample;
+  float clip_range;
+  int use_clipped_model_output, num_train_timesteps;
+  void* prev;
+  void* x0;
+  int out_dtype;
+} ldm_unet_tail_params;
+
+int ldm_unet_tail(const ldm_unet_tail_params* p, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * ldm_linear_rows — out[m][:] = act(x[m] . W^T + bias) for rows <= 16 (the time-embedding MLP:
  * diffusers TimestepEmbedding linear_1 / linear_2 and the batched ResnetBlock2D time_emb_proj,
  * unet.py:301-307 and every resnet's temb input).  x bf16 [rows][k]; x == NULL takes the row

@@ -192,6 +192,54 @@ def gn_case(B, HW, C, stats):
     return run, None, (2 + (0 if stats else 1)) * x.numel() * 2
 
 
+def tail_case(B, fused=True, ddim=True):
+    """The UNet tail at the 64x64 level: GroupNorm -> SiLU -> conv_out (320 -> 4) (-> DDIM), as one
+    ldm_unet_tail launch or the group_norm + conv2d (NCHW) + ddim_step launches it replaces."""
+    C, H, G = 320, 64, 32
+    B = max(1, B * BATCH // 8)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    xr = torch.randn(B, H, H, C, device=DEV, generator=g).to(BF)
+    pid = K.PackedConv(torch.eye(C, device=DEV)[:, :, None, None], torch.zeros(C, device=DEV), BF)
+    x = K.conv2d(pid, xr, B, H, H, gn_stats=True)
+    gam, bet = torch.rand(C, device=DEV) + 0.5, torch.randn(C, device=DEV) * 0.1
+    pc = K.PackedConv(torch.randn(4, C, 3, 3, device=DEV, generator=g) * 0.02, torch.randn(4, device=DEV), BF)
+    smp = torch.randn(B, 4, H, H, device=DEV)
+    ac = torch.linspace(0.9999, 0.005, 1000, device=DEV)
+    t = torch.tensor([741], dtype=torch.int64, device=DEV)
+    d = dict(sample=smp, t=t, alphas_cumprod=ac, final_alpha=1.0, step_ratio=20, prediction_type="epsilon",
+             clip_sample=False, clip_range=1.0, use_clipped=False, out_dtype=torch.float32)
+
+    def run():
+        if fused:
+            return K.unet_tail(x, B, H, H, G, gam, bet, 1e-5, pc, BF, ddim=d if ddim else None, want_eps=not ddim)
+        h = K.group_norm(x, B, H * H, G, gam, bet, 1e-5, K.ACT_SILU)
+        e = K.conv2d(pc, h, B, H, H, out_layout=K.OUT_NCHW)
+        return K.ddim_step(e, smp, t, ac, 1.0, 20, "epsilon", False, 1.0, False, torch.float32) if ddim else e
+    return run, None, x.numel() * 2
+
+
+def temb_case(B, fused=True):
+    """The time-embedding MLP: sinusoid -> linear_1 + SiLU -> linear_2 + SiLU -> the 22 batched
+    time_emb_proj (1280 -> 20160), as ldm_linear_rows launches or the tproj + tile-GEMM path."""
+    g = torch.Generator(device=DEV).manual_seed(0)
+    l1 = K.PackedConv(torch.randn(1280, 320, device=DEV, generator=g) * 0.05, torch.randn(1280, device=DEV), BF)
+    l2 = K.PackedConv(torch.randn(1280, 1280, device=DEV, generator=g) * 0.03, torch.randn(1280, device=DEV), BF)
+    tp = K.PackedConv(torch.randn(20160, 1280, device=DEV, generator=g) * 0.03, torch.randn(20160, device=DEV), BF)
+    freqs = torch.exp(-torch.log(torch.tensor(10000.0)) * torch.arange(160) / 160).to(DEV)
+    t = torch.tensor([741.0], device=DEV)
+
+    def run():
+        if fused:
+            e = K.linear_rows(l1, None, B, act=K.ACT_SILU, t=t, freqs=freqs)
+            e = K.linear_rows(l2, e, B, act=K.ACT_SILU)
+            return K.linear_rows(tp, e, B, out_dtype=torch.float32)
+        e = K.timestep_proj(t, B, freqs, 320, True, BF)
+        e = K.linear(l1, e, act=K.ACT_SILU)
+        e = K.linear(l2, e, act=K.ACT_SILU)
+        return K.linear(tp, e, out_dtype=torch.float32)
+    return run, None, (tp.w.numel() + l1.w.numel() + l2.w.numel()) * 2
+
+
 def ln_case(rows, C):
     x = torch.randn(rows, C, device=DEV).to(BF)
     gam, bet = torch.ones(C, device=DEV), torch.zeros(C, device=DEV)
@@ -363,6 +411,11 @@ CASES = {
     "gn_l3_fused": lambda: gn_case(8, 64, 1280, True),
     "gn_up0_fused": lambda: gn_case(8, 4096, 960, True),
     "ln_l0": lambda: ln_case(32768, 320),
+    "tail_l0": lambda: tail_case(8),
+    "tail_l0_eps": lambda: tail_case(8, ddim=False),
+    "tail_l0_unfused": lambda: tail_case(8, fused=False),
+    "temb_mlp": lambda: temb_case(8),
+    "temb_mlp_unfused": lambda: temb_case(8, fused=False),
     "panoptic_k128_512": lambda: panoptic_case(8, 128, 512, 512),
     "panoptic_k30_512": lambda: panoptic_case(8, 30, 512, 512),
     "ln_l1": lambda: ln_case(8192, 640),

@@ -136,6 +136,32 @@ __device__ __forceinline__ void glds16(const void* gsrc, unsigned lds_addr) {
       : "memory");
 }
 
+// DDIM step arithmetic (ddim_scheduler.py:218-269), shared by ldm_ddim_step and the fused UNet tail:
+// coefficients of timestep t (ac = alphas_cumprod, NaN for an out-of-range t, never an OOB read) and
+// the per-element update.
+struct DdimCoef { float sa, sb, sap, sbp; };
+__device__ __forceinline__ float ddim_table_at(const float* ac, int64_t t, int ntrain) {
+  return (t >= 0 && t < ntrain) ? ac[t] : __int_as_float(0x7fc00000);
+}
+__device__ __forceinline__ DdimCoef ddim_coef(const float* ac, int64_t t, int step_ratio, float final_ac, int ntrain) {
+  const int64_t pt = t - step_ratio;
+  const float at = ddim_table_at(ac, t, ntrain);
+  const float ap = pt >= 0 ? ddim_table_at(ac, pt, ntrain) : final_ac;
+  const float bt = 1.0f - at;
+  return DdimCoef{sqrtf(at), sqrtf(bt), sqrtf(ap), sqrtf(1.0f - ap)};
+}
+// m = model output, x = sample -> (prev_sample, pred_original_sample)
+__device__ __forceinline__ float2 ddim_apply(const DdimCoef& c, float m, float x, int pred, int clip, float clip_range,
+                                             int use_clipped) {
+  float x0, eps;
+  if (pred == LDM_PRED_EPSILON) { x0 = (x - c.sb * m) / c.sa; eps = m; }
+  else if (pred == LDM_PRED_SAMPLE) { x0 = m; eps = (x - c.sa * x0) / c.sb; }
+  else { x0 = c.sa * x - c.sb * m; eps = c.sa * m + c.sb * x; }
+  if (clip) x0 = fminf(fmaxf(x0, -clip_range), clip_range);
+  if (use_clipped) eps = (x - c.sa * x0) / c.sb;
+  return make_float2(c.sap * x0 + c.sbp * eps, x0);
+}
+
 #define LDM_CHECK_LAUNCH()                                   \
   do {                                                       \
     hipError_t _e = hipGetLastError();                       \

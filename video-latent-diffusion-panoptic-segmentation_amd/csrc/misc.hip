@@ -79,18 +79,29 @@ __global__ __launch_bounds__(256) void linear_rows_kernel(const bf16_t* __restri
         xa[i] = lr < rows ? *reinterpret_cast<const uint4*>(x + (int64_t)lr * k + (s0 + i) * 32 + 8 * g)
                           : make_uint4(0u, 0u, 0u, 0u);
   } else {
+    // every frequency load of this lane in flight before the first sin / cos (8 consecutive j never
+    // straddle the sin / cos halves: half % 8 == 0, checked on the host)
     const int half = k / 2;
     const float tv = lr < rows ? t[n_t == 1 ? 0 : lr] : 0.f;
+    float4 fq[LR_MAXS][2];
 #pragma unroll
     for (int i = 0; i < LR_MAXS; ++i) {
       if (s0 + i >= s1) continue;
+      const int j0 = (s0 + i) * 32 + 8 * g;
+      const float* fp = freqs + (j0 < half ? j0 : j0 - half);
+      fq[i][0] = *reinterpret_cast<const float4*>(fp);
+      fq[i][1] = *reinterpret_cast<const float4*>(fp + 4);
+    }
+#pragma unroll
+    for (int i = 0; i < LR_MAXS; ++i) {
+      if (s0 + i >= s1) continue;
+      const int j0 = (s0 + i) * 32 + 8 * g;
+      const bool use_cos = flip ? j0 < half : j0 >= half;   // [sin || cos], flipped to [cos || sin]
+      const float f[8] = {fq[i][0].x, fq[i][0].y, fq[i][0].z, fq[i][0].w, fq[i][1].x, fq[i][1].y, fq[i][1].z, fq[i][1].w};
       bf16_t h[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int j = (s0 + i) * 32 + 8 * g + e;
-        const bool first = j < half;
-        const float arg = tv * freqs[first ? j : j - half];
-        const bool use_cos = flip ? first : !first;          // [sin || cos], flipped to [cos || sin]
+        const float arg = tv * f[e];
         h[e] = lr < rows ? f2bf(use_cos ? cosf(arg) : sinf(arg)) : (bf16_t)0;
       }
       xa[i] = *reinterpret_cast<const uint4*>(h);
@@ -138,30 +149,15 @@ struct DdimArgs {
   int ntrain;
 };
 
-__device__ __forceinline__ float table_at(const float* ac, int64_t t, int ntrain) {
-  return (t >= 0 && t < ntrain) ? ac[t] : __int_as_float(0x7fc00000);  // NaN, never an OOB read
-}
+__device__ __forceinline__ float table_at(const float* ac, int64_t t, int ntrain) { return ddim_table_at(ac, t, ntrain); }
 
 __global__ void ddim_step_kernel(const DdimArgs a) {
-  const int64_t t = *a.t;
-  const int64_t pt = t - a.step_ratio;
-  const float at = table_at(a.ac, t, a.ntrain);
-  const float ap = pt >= 0 ? table_at(a.ac, pt, a.ntrain) : a.final_ac;
-  const float bt = 1.0f - at;
-  const float sa = sqrtf(at), sb = sqrtf(bt);
-  const float sap = sqrtf(ap), sbp = sqrtf(1.0f - ap);
+  const DdimCoef c = ddim_coef(a.ac, *a.t, a.step_ratio, a.final_ac, a.ntrain);
   for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * 256) {
-    const float m = ld_dt(a.mo, i, a.mo_dt);
-    const float x = ld_dt(a.x, i, a.x_dt);
-    float x0, eps;
-    if (a.pred == LDM_PRED_EPSILON) { x0 = (x - sb * m) / sa; eps = m; }
-    else if (a.pred == LDM_PRED_SAMPLE) { x0 = m; eps = (x - sa * x0) / sb; }
-    else { x0 = sa * x - sb * m; eps = sa * m + sb * x; }
-    if (a.clip) x0 = fminf(fmaxf(x0, -a.clip_range), a.clip_range);
-    if (a.use_clipped) eps = (x - sa * x0) / sb;
-    const float prev = sap * x0 + sbp * eps;
-    if (a.prev) st_dt(a.prev, i, prev, a.out_dt);
-    if (a.x0) st_dt(a.x0, i, x0, a.out_dt);
+    const float2 r = ddim_apply(c, ld_dt(a.mo, i, a.mo_dt), ld_dt(a.x, i, a.x_dt), a.pred, a.clip, a.clip_range,
+                                a.use_clipped);
+    if (a.prev) st_dt(a.prev, i, r.x, a.out_dt);
+    if (a.x0) st_dt(a.x0, i, r.y, a.out_dt);
   }
 }
 
@@ -287,7 +283,7 @@ extern "C" int ldm_linear_rows(const void* x, const float* t, int n_t, const flo
   if (!w || !out || rows <= 0 || rows > 16 || n <= 0 || n % 16 || k <= 0 || k % 32 || k > kpad || kpad % 8) return LDM_ERR_ARG;
   if (k > 4 * 32 * LR_MAXS || (out_dtype != LDM_F32 && out_dtype != LDM_BF16)) return LDM_ERR_ARG;
   if (act < LDM_ACT_NONE || act > LDM_ACT_SIGMOID) return LDM_ERR_ARG;
-  if (!x && (!t || !freqs || k % 2 || (n_t != 1 && n_t != rows))) return LDM_ERR_ARG;
+  if (!x && (!t || !freqs || k % 16 || (n_t != 1 && n_t != rows) || !aligned16(freqs))) return LDM_ERR_ARG;
   if ((x && !aligned16(x)) || !aligned16(w) || !aligned16(out) || (reinterpret_cast<uintptr_t>(out) & 15)) return LDM_ERR_ALIGN;
   hipLaunchKernelGGL(linear_rows_kernel, dim3(n / 16), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      reinterpret_cast<const bf16_t*>(x), t, n_t, freqs, flip, reinterpret_cast<const bf16_t*>(w), kpad,

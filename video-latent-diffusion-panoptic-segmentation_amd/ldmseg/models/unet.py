@@ -666,7 +666,23 @@ class UNet(nn.Module):
         with K.gn_arena(("unet", id(self), tuple(s0.shape), self.compute_dtype), s0.device):
             return self._forward_sources(sources, timestep, encoder_hidden_states)
 
-    def _forward_sources(self, sources, timestep, encoder_hidden_states=None):
+    @torch.no_grad()
+    def forward_ddim_step(self, sources, timestep, scheduler, t_int, sample, encoder_hidden_states=None):
+        """One sampler step, trainers_ldm_cond.py:1144-1162: eps = unet(cat(sources), t) and
+        scheduler.step(eps, t, sample) -> (prev_sample, pred_original_sample).  On the bf16 path the
+        step runs inside the UNet tail's launch (ldm_unet_tail: GroupNorm -> SiLU -> conv_out -> DDIM
+        on the same device arithmetic as ldm_ddim_step, the model output rounded to bf16 first, as the
+        unfused conv stores it); otherwise the two calls."""
+        s0 = sources[0]
+        ddim = scheduler.fused_step_args(t_int, sample, self.compute_dtype)
+        with K.gn_arena(("unet", id(self), tuple(s0.shape), self.compute_dtype), s0.device):
+            r = self._forward_sources(sources, timestep, encoder_hidden_states, ddim=ddim)
+        if isinstance(r, tuple):
+            return r[1], r[2]
+        out = scheduler.step(r, t_int, sample)
+        return out.prev_sample, out.pred_original_sample
+
+    def _forward_sources(self, sources, timestep, encoder_hidden_states=None, ddim=None):
         P = self.prepare()
         dt = self.compute_dtype
         sample = sources[0]
@@ -721,9 +737,22 @@ class UNet(nn.Module):
             if blk.upsamplers is not None:
                 x = K.conv2d(P[id(blk.upsamplers[0])], x, B, H, W, upsample=True, gn_stats=True)
                 H, W = 2 * H, 2 * W
-        x = K.group_norm(x, B, H * W, self.conv_norm_out.num_groups, *P["out_norm"], self.conv_norm_out.eps,
-                         K.ACT_SILU)
+        G = self.conv_norm_out.num_groups
+        if self.tail_fused and K.unet_tail_ok(x, B, H, W, G, P["conv_out"]):
+            # conv_norm_out -> SiLU -> conv_out (-> the sampler's DDIM step) in one launch
+            return K.unet_tail(x, B, H, W, G, *P["out_norm"], self.conv_norm_out.eps, P["conv_out"], dt, ddim=ddim,
+                               want_eps=False)
+        x = K.group_norm(x, B, H * W, G, *P["out_norm"], self.conv_norm_out.eps, K.ACT_SILU)
         return K.conv2d(P["conv_out"], x, B, H, W, out_layout=K.OUT_NCHW)
+
+    @property
+    def tail_fused(self):
+        return getattr(self, "_tail_fused", True)
+
+    def set_tail_fused(self, enabled=True):
+        """bf16: run conv_norm_out -> SiLU -> conv_out (and, in forward_ddim_step, the DDIM step) as
+        one ldm_unet_tail launch (default on); off runs ldm_group_norm + ldm_conv2d (+ ldm_ddim_step)."""
+        self._tail_fused = bool(enabled)
 
 
 class _UNetTrainFn(torch.autograd.Function):

@@ -49,6 +49,16 @@ class AttnParams(ctypes.Structure):
                 ("n_q", _i), ("n_kv", _i), ("scale", _f), ("dtype", _i)]
 
 
+class UnetTailParams(ctypes.Structure):
+    _fields_ = [("h", _vp), ("batch", _i), ("height", _i), ("width", _i), ("c", _i), ("gn_acc", _vp),
+                ("gn_unit", _i), ("gn_slots", _i), ("groups", _i), ("eps", _f), ("gamma", _vp), ("beta", _vp),
+                ("w", _vp), ("kpad", _i), ("cout", _i), ("bias", _vp), ("eps_out", _vp), ("eps_dtype", _i),
+                ("sample", _vp), ("sample_dtype", _i), ("t", _vp), ("alphas_cumprod", _vp),
+                ("final_alpha_cumprod", _f), ("step_ratio", _i), ("prediction_type", _i), ("clip_sample", _i),
+                ("clip_range", _f), ("use_clipped_model_output", _i), ("num_train_timesteps", _i), ("prev", _vp),
+                ("x0", _vp), ("out_dtype", _i)]
+
+
 class WgradParams(ctypes.Structure):
     _fields_ = [("a0", _vp), ("a1", _vp), ("c0", _i), ("c1", _i), ("batch", _i), ("h_in", _i), ("w_in", _i),
                 ("h_out", _i), ("w_out", _i), ("ksize", _i), ("stride", _i), ("upsample", _i), ("dy", _vp),
@@ -90,6 +100,7 @@ EXPORTS = {
     "ldm_group_norm": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _f, _i, _vp, _vp, _vp, _i, _i, _vp, _i, _vp]),
     "ldm_layer_norm": (_i, [_vp, _i, _i, _vp, _vp, _f, _i, _vp, _i, _vp]),
     "ldm_timestep_proj": (_i, [_vp, _i, _i, _vp, _i, _i, _vp, _i, _vp]),
+    "ldm_unet_tail": (_i, [ctypes.POINTER(UnetTailParams), _vp]),
     "ldm_linear_rows": (_i, [_vp, _vp, _i, _vp, _i, _vp, _i, _i, _i, _vp, _i, _i, _vp, _i, _vp]),
     "ldm_ddim_step": (_i, [ctypes.POINTER(DdimParams), _vp]),
     "ldm_ddim_add_noise": (_i, [_vp, _vp, _vp, _vp, _i, _f, _i, _i64, _vp, _i, _vp]),
@@ -1005,6 +1016,56 @@ def linear_rows(pc: PackedConv, x, rows, *, act=ACT_NONE, out_dtype=None, t=None
                                _ptr(pc.w), pc.kpad, pc.cin, pc.n, _ptr(pc.bias), rows, act, _ptr(out),
                                dtype_code(out_dtype), _stream(pc.w)), "ldm_linear_rows")
     return out
+
+
+def unet_tail_ok(x, batch, h, w, groups, pc: PackedConv):
+    """ldm_unet_tail takes this GroupNorm -> SiLU -> conv_out (bf16 input with producer statistics)."""
+    st = gn_stats_of(x)
+    if x.dtype != torch.bfloat16 or pc.dtype != torch.bfloat16 or pc.ksize != 3 or pc.n > 4 or st is None:
+        return False
+    c = pc.cin
+    unit, slots = c // st.shape[2], st.shape[1]
+    return (x.is_contiguous() and x.numel() == batch * h * w * c and h % 2 == 0 and w % 16 == 0 and w <= 64
+            and c % 64 == 0 and c <= 640 and 0 < groups <= 64 and c % groups == 0 and (c // groups) % unit == 0
+            and slots * (c // unit) <= 1024 and pc.bias is not None)
+
+
+def unet_tail(x, batch, h, w, groups, gamma, beta, eps, pc: PackedConv, eps_dtype, ddim=None, want_eps=True):
+    """GroupNorm(conv_norm_out) -> SiLU -> conv_out in one launch (ldm_unet_tail), x NHWC [batch, h, w, c]
+    with producer GroupNorm statistics.  Returns the NCHW model output [batch, cout, h, w] in eps_dtype,
+    or with ``ddim`` = dict(sample, t, alphas_cumprod, final_alpha, step_ratio, prediction_type,
+    clip_sample, clip_range, use_clipped, out_dtype) the DDIM step on it fused: (eps | None, prev, x0)."""
+    lib = load_library()
+    st = gn_stats_of(x)
+    _gpu(x, gamma, beta, pc.w, st)
+    c = pc.cin
+    unit, slots = c // st.shape[2], st.shape[1]
+    eps_out = torch.empty(batch, pc.n, h, w, dtype=eps_dtype, device=x.device) if (want_eps or ddim is None) else None
+    prev = x0 = None
+    d = ddim or {}
+    if ddim is not None:
+        smp = d["sample"]
+        _gpu(smp, d["t"], d["alphas_cumprod"])
+        _contig(smp, "sample")
+        if smp.shape != (batch, pc.n, h, w) or d["t"].dtype != torch.int64 or d["t"].numel() != 1:
+            raise ValueError("ddim sample must be NCHW [batch, cout, h, w] and t one int64 device element")
+        prev = torch.empty(smp.shape, dtype=d["out_dtype"], device=x.device)
+        x0 = torch.empty(smp.shape, dtype=d["out_dtype"], device=x.device)
+    p = UnetTailParams(_ptr(x), batch, h, w, c, _ptr(st), unit, slots, groups, float(eps), _ptr(gamma), _ptr(beta),
+                       _ptr(pc.w), pc.kpad, pc.n, _ptr(pc.bias), _ptr(eps_out), dtype_code(eps_dtype),
+                       _ptr(d.get("sample")), dtype_code(d["sample"].dtype) if ddim else 0, _ptr(d.get("t")),
+                       _ptr(d.get("alphas_cumprod")), float(d.get("final_alpha", 0.0)), int(d.get("step_ratio", 0)),
+                       PRED[d.get("prediction_type", "epsilon")], int(d.get("clip_sample", 0)),
+                       float(d.get("clip_range", 0.0)), int(d.get("use_clipped", 0)),
+                       d["alphas_cumprod"].numel() if ddim else 0, _ptr(prev), _ptr(x0),
+                       dtype_code(d["out_dtype"]) if ddim else 0)
+    ev = _prof_start()
+    _check(lib.ldm_unet_tail(ctypes.byref(p), _stream(x)), "ldm_unet_tail")
+    _prof_stop(ev, "igemm", 2.0 * batch * h * w * pc.n * 9 * c, x.numel() * x.element_size(),
+               f"tail M={batch * h * w} C={c} N={pc.n}")
+    if ddim is None:
+        return eps_out
+    return eps_out, prev, x0
 
 
 def timestep_proj(t_f32, batch, freqs, dim, flip_sin_to_cos, dtype):

@@ -47,6 +47,9 @@ class DenoiseStep:
 
     def _body(self):
         srcs = [self.lat, self.rgb] + ([self.cond] if self.cond is not None else [])   # conv_in gather casts
+        if hasattr(self.unet, "forward_ddim_step"):
+            # UNet + scheduler.step, the step fused into the UNet tail's launch where it can be
+            return self.unet.forward_ddim_step(srcs, self.t_f, self.sched, self.t_int, self.lat)
         eps = self.unet.forward_sources(srcs, self.t_f)
         r = self.sched.step(eps, self.t_int, self.lat)
         return r.prev_sample, r.pred_original_sample
