@@ -339,7 +339,7 @@ int ldm_unet_tail(const ldm_unet_tail_params* p, ldm_stream_t stream);
  * ldm_linear_rows — out[m][:] = act(x[m] . W^T + bias) for rows <= 16 (the time-embedding MLP:
  * diffusers TimestepEmbedding linear_1 / linear_2 and the batched ResnetBlock2D time_emb_proj,
  * unet.py:301-307 and every resnet's temb input).  x bf16 [rows][k]; x == NULL takes the row
- * as the sinusoidal projection of t (the ldm_timestep_proj values rounded to bf16, dim = k).
+ * as the sinusoidal projection of t (the ldm_timestep_proj values rounded to bf16, dim = k <= 512).
  * W packed bf16 [n][kpad] (n % 16 == 0, k % 32 == 0, k <= 1536), bias fp32 [n] or NULL,
  * out [rows][n] fp32 or bf16 (16-byte aligned).
  * ------------------------------------------------------------------------------------- */

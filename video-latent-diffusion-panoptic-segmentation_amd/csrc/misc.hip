@@ -55,6 +55,7 @@ __global__ void tproj_kernel(const float* __restrict__ t, int n_t, int batch, co
 // tiles are summed in a fixed order through LDS.  x == NULL: the input row is the sinusoidal timestep
 // projection (diffusers Timesteps, the tproj_kernel values rounded to bf16) computed in place.
 constexpr int LR_MAXS = 12;   // k32 steps per wave held in registers (K <= 4 * 32 * 12 = 1536)
+constexpr int LR_SIN_MAXK = 512;   // sinusoid width formed in LDS
 
 __global__ __launch_bounds__(256) void linear_rows_kernel(const bf16_t* __restrict__ x, const float* __restrict__ t,
                                                           int n_t, const float* __restrict__ freqs, int flip,
@@ -62,6 +63,7 @@ __global__ __launch_bounds__(256) void linear_rows_kernel(const bf16_t* __restri
                                                           const float* __restrict__ bias, int rows, int act, void* out,
                                                           int out_dt) {
   __shared__ f32x4_t part[3][64];
+  __shared__ __attribute__((aligned(16))) bf16_t xs[16 * LR_SIN_MAXK];   // the sinusoid rows (x == NULL)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int lr = lane & 15, g = lane >> 4;
   const int n0 = blockIdx.x * 16;
@@ -79,33 +81,22 @@ __global__ __launch_bounds__(256) void linear_rows_kernel(const bf16_t* __restri
         xa[i] = lr < rows ? *reinterpret_cast<const uint4*>(x + (int64_t)lr * k + (s0 + i) * 32 + 8 * g)
                           : make_uint4(0u, 0u, 0u, 0u);
   } else {
-    // every frequency load of this lane in flight before the first sin / cos (8 consecutive j never
-    // straddle the sin / cos halves: half % 8 == 0, checked on the host)
+    // the sinusoid rows, one value per thread at a time into LDS (sin / cos of arguments up to ~1e3
+    // take ocml's slow range reduction: 24 of them serially per lane cost ~12 us), then the fragments
     const int half = k / 2;
-    const float tv = lr < rows ? t[n_t == 1 ? 0 : lr] : 0.f;
-    float4 fq[LR_MAXS][2];
-#pragma unroll
-    for (int i = 0; i < LR_MAXS; ++i) {
-      if (s0 + i >= s1) continue;
-      const int j0 = (s0 + i) * 32 + 8 * g;
-      const float* fp = freqs + (j0 < half ? j0 : j0 - half);
-      fq[i][0] = *reinterpret_cast<const float4*>(fp);
-      fq[i][1] = *reinterpret_cast<const float4*>(fp + 4);
+    for (int e = threadIdx.x; e < rows * k; e += 256) {
+      const int r = e / k, j = e - r * k;
+      const bool first = j < half;
+      const float arg = t[n_t == 1 ? 0 : r] * freqs[first ? j : j - half];
+      const bool use_cos = flip ? first : !first;            // [sin || cos], flipped to [cos || sin]
+      xs[e] = f2bf(use_cos ? cosf(arg) : sinf(arg));
     }
+    __syncthreads();
 #pragma unroll
-    for (int i = 0; i < LR_MAXS; ++i) {
-      if (s0 + i >= s1) continue;
-      const int j0 = (s0 + i) * 32 + 8 * g;
-      const bool use_cos = flip ? j0 < half : j0 >= half;   // [sin || cos], flipped to [cos || sin]
-      const float f[8] = {fq[i][0].x, fq[i][0].y, fq[i][0].z, fq[i][0].w, fq[i][1].x, fq[i][1].y, fq[i][1].z, fq[i][1].w};
-      bf16_t h[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float arg = tv * f[e];
-        h[e] = lr < rows ? f2bf(use_cos ? cosf(arg) : sinf(arg)) : (bf16_t)0;
-      }
-      xa[i] = *reinterpret_cast<const uint4*>(h);
-    }
+    for (int i = 0; i < LR_MAXS; ++i)
+      if (s0 + i < s1)
+        xa[i] = lr < rows ? *reinterpret_cast<const uint4*>(xs + lr * k + (s0 + i) * 32 + 8 * g)
+                          : make_uint4(0u, 0u, 0u, 0u);
   }
   f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -283,7 +274,7 @@ extern "C" int ldm_linear_rows(const void* x, const float* t, int n_t, const flo
   if (!w || !out || rows <= 0 || rows > 16 || n <= 0 || n % 16 || k <= 0 || k % 32 || k > kpad || kpad % 8) return LDM_ERR_ARG;
   if (k > 4 * 32 * LR_MAXS || (out_dtype != LDM_F32 && out_dtype != LDM_BF16)) return LDM_ERR_ARG;
   if (act < LDM_ACT_NONE || act > LDM_ACT_SIGMOID) return LDM_ERR_ARG;
-  if (!x && (!t || !freqs || k % 16 || (n_t != 1 && n_t != rows) || !aligned16(freqs))) return LDM_ERR_ARG;
+  if (!x && (!t || !freqs || k % 2 || k > LR_SIN_MAXK || (n_t != 1 && n_t != rows))) return LDM_ERR_ARG;
   if ((x && !aligned16(x)) || !aligned16(w) || !aligned16(out) || (reinterpret_cast<uintptr_t>(out) & 15)) return LDM_ERR_ALIGN;
   hipLaunchKernelGGL(linear_rows_kernel, dim3(n / 16), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
                      reinterpret_cast<const bf16_t*>(x), t, n_t, freqs, flip, reinterpret_cast<const bf16_t*>(w), kpad,

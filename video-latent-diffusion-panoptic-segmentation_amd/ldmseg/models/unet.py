@@ -696,8 +696,8 @@ class UNet(nn.Module):
         if not torch.is_tensor(timestep):
             timestep = torch.tensor([timestep], device=dev)
         t = timestep.reshape(-1).to(device=dev, dtype=torch.float32)
-        if dt == torch.bfloat16 and P["lin1"].cin == self.time_proj.num_channels and all(
-                K.linear_rows_ok(P[k], B) for k in ("lin1", "lin2", "temb_proj")):
+        if dt == torch.bfloat16 and P["lin1"].cin == self.time_proj.num_channels and \
+                K.linear_rows_ok(P["lin1"], B, sinusoid=True) and all(K.linear_rows_ok(P[k], B) for k in ("lin2", "temb_proj")):
             # few-row GEMMs that stream each weight once (ldm_linear_rows); the sinusoid is formed
             # inside linear_1's launch
             emb = K.linear_rows(P["lin1"], None, B, act=K.ACT_SILU, t=t, freqs=P["freqs"],

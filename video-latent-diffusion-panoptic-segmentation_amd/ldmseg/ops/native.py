@@ -995,11 +995,11 @@ def layer_norm(x, gamma, beta, eps, act=ACT_NONE, out=None):
     return out
 
 
-def linear_rows_ok(pc: PackedConv, rows, x=None):
-    """ldm_linear_rows takes this bf16 linear over `rows` (<= 16) rows."""
+def linear_rows_ok(pc: PackedConv, rows, x=None, sinusoid=False):
+    """ldm_linear_rows takes this bf16 linear over `rows` (<= 16) rows (sinusoid input: k <= 512)."""
     k = pc.cin
     return (pc.dtype == torch.bfloat16 and pc.ksize == 1 and 0 < rows <= 16 and pc.n % 16 == 0 and k % 32 == 0
-            and k <= 1536 and (x is None or (x.dtype == torch.bfloat16 and x.is_contiguous())))
+            and k <= (512 if sinusoid else 1536) and (x is None or (x.dtype == torch.bfloat16 and x.is_contiguous())))
 
 
 def linear_rows(pc: PackedConv, x, rows, *, act=ACT_NONE, out_dtype=None, t=None, freqs=None, flip_sin_to_cos=True):
