@@ -859,37 +859,51 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
   // row bases; at the odd tap shifts it averaged 1.67 LDS cycles per group)
   // does this wave issue a halo piece at tap `tap` (for the next channel block)?
   auto has_piece = [&](int tap) { return tap < A_TAPS && tap * PIECES_PER_TAP + wv < NP; };
-  auto issue_halo = [&](int cb, int tap) {
-    const int j = tap * PIECES_PER_TAP + wv;
-    const int slot = j * 64 + lane;
+  // Everything per-lane in the operand addressing is fixed for the whole launch, so it is computed
+  // once here: the lane's source offset of each of its halo pieces (per source of a concat; the
+  // channel block enters as a wave-uniform soffset), the row offsets of its B rows (the K position
+  // enters as soffset), and the LDS byte offset of every A fragment at every tap (the swizzle
+  // c ^ (hp & 7) moves with the tap shift, so the 9 x FM offsets are precomputed; ks = 1 is ^ 64).
+  // The main loop then spends no VALU on addresses beyond one add per fragment read.
+  int hoff0[A_TAPS], hoff1[A_TAPS];
+#pragma unroll
+  for (int t = 0; t < A_TAPS; ++t) {
+    const int jj = t * PIECES_PER_TAP + wv;
+    const int slot = jj * 64 + lane;
     const int hp = slot >> 3, sp = slot & 7;
     const int c = sp ^ (hp & 7);
     const int hr = hp / HW, hx = hp - hr * HW;
     const int iy = oy0 - 1 + hr, ix = hx - 1;
-    const bool src1 = p.c1 > 0 && cb * 64 >= p.c0;            // uniform per channel block
-    const int cs = src1 ? p.c1 : p.c0;
-    const int ch = cb * 64 - (src1 ? p.c0 : 0) + 8 * c;
     const bool ok = hp < HPIX && (unsigned)iy < (unsigned)p.h_in && (unsigned)ix < (unsigned)W;
-    const int off = ok ? (((b * p.h_in + iy) * W + ix) * cs + ch) * 2 : kOOB;
+    const int pix = (b * p.h_in + iy) * W + ix;
+    hoff0[t] = ok ? (pix * p.c0 + 8 * c) * 2 : kOOB;
+    hoff1[t] = ok ? (pix * (p.c1 > 0 ? p.c1 : 1) + 8 * c) * 2 : kOOB;
+  }
+  auto issue_halo = [&](int cb, int tap) {
+    const int j = tap * PIECES_PER_TAP + wv;
+    const bool src1 = p.c1 > 0 && cb * 64 >= p.c0;            // uniform per channel block
+    const int soff = __builtin_amdgcn_readfirstlane((cb * 64 - (src1 ? p.c0 : 0)) * 2);
     const unsigned dst = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)(((cb & 1) * HALO_U4 + j * 64) * 16));
-    if (src1) dma16(ra1, off, dst);
-    else dma16(ra0, off, dst);
+    if (src1) dma16s(ra1, hoff1[tap], soff, dst);
+    else dma16s(ra0, hoff0[tap], soff, dst);
   };
-  // B tile of step s: rows n0 + r (r < 160), packed-K columns tap * cin + cb * 64 .. + 64;
+  // B tile of step (cb, tap): rows n0 + r (r < 160), packed-K columns tap * cin + cb * 64 .. + 64;
   // waves 0-3 load rows rr, rr + 64, rr + 128 (rr < 32 for the last), waves 4-7 two
   const int rr = tid >> 3, cc = tid & 7;               // rr in [0, 64)
   const int cl = cc ^ ((rr >> 1) & 7);                 // (rr + 64 i) >> 1 & 7 == rr >> 1 & 7
-  auto issue_b = [&](int s) {
-    const int cb = cb0 + s / 9, tap = s - 9 * (s / 9);
-    const int kb = (tap * p.cin + cb * 64 + 8 * cl) * 2;
-    const unsigned base = lds_b + (unsigned)((s % NBS) * B_U4 * 16);
+  int boff[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int r = rr + 64 * i, n = n0 + r;
+    boff[i] = (r < BN && n < p.n) ? (n * p.kpad + 8 * cl) * 2 : kOOB;
+  }
+  auto issue_b = [&](int cb, int tap, int slotb) {
+    const int soff = __builtin_amdgcn_readfirstlane((tap * p.cin + cb * 64) * 2);
+    const unsigned base = lds_b + (unsigned)(slotb * B_U4 * 16);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       if (i == 2 && wv >= 4) break;
-      const int r = rr + 64 * i;
-      const int n = n0 + r;
-      const int off = (r < BN && n < p.n) ? n * p.kpad * 2 + kb : kOOB;
-      dma16(rw, off, __builtin_amdgcn_readfirstlane(base + (unsigned)((64 * i + 8 * wv) * 128)));
+      dma16s(rw, boff[i], soff, __builtin_amdgcn_readfirstlane(base + (unsigned)((64 * i + 8 * wv) * 128)));
     }
   };
 
@@ -899,33 +913,39 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // per-fragment halo pixel of this lane at tap (0, 0)
-  int hp0[FM];
+  // LDS byte offset of A fragment i at tap t (k32 half 0; half 1 is ^ 64), buffer 0
+  int aoff[9][FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int ml = wm * WT + 16 * i + lr;
     const int oyl = ml / W, ox = ml - oyl * W;
-    hp0[i] = oyl * HW + ox;
+    const int hp0 = oyl * HW + ox;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int hp = hp0 + (t / 3) * HW + (t % 3);
+      aoff[t][i] = hp * 128 + ((g ^ (hp & 7)) << 4);
+    }
   }
-  auto compute = [&](int s) {
-    const int cb = cb0 + s / 9, tap = s - 9 * (s / 9);
-    const int ky = tap / 3, kx = tap - 3 * ky;
-    const uint4* As = smem + (cb & 1) * HALO_U4;
-    const uint4* Bs = smem + 2 * HALO_U4 + (s % NBS) * B_U4;
-    const int toff = ky * HW + kx;
+  // B fragment offsets (uint4 units), fixed per (j, ks)
+  int boffr[2][FN];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int r = wn * 80 + j * 16 + lr;
+      boffr[ks][j] = r * 8 + swz(r, ks * 4 + g);
+    }
+  const char* smem_c = reinterpret_cast<const char*>(smem);
+  auto compute = [&](int tap, int abuf, int bslot) {
+    const uint4* Bs = smem + 2 * HALO_U4 + bslot * B_U4;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       Frag8<T> af[FM], bfr[FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const int hp = hp0[i] + toff;
-        af[i].v = As[hp * 8 + ((ks * 4 + g) ^ (hp & 7))];
-      }
+      for (int i = 0; i < FM; ++i)
+        af[i].v = *reinterpret_cast<const uint4*>(smem_c + ((aoff[tap][i] ^ (ks << 6)) + abuf));
 #pragma unroll
-      for (int j = 0; j < FN; ++j) {
-        const int r = wn * 80 + j * 16 + lr;
-        bfr[j].v = Bs[r * 8 + swz(r, ks * 4 + g)];
-      }
+      for (int j = 0; j < FN; ++j) bfr[j].v = Bs[boffr[ks][j]];
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -937,23 +957,31 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
 #pragma unroll
   for (int t = 0; t < A_TAPS; ++t)
     if (has_piece(t)) issue_halo(cb0, t);
-  issue_b(0);
+  issue_b(cb0, 0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
-    const int cb = cb0 + s / 9, tap = s - 9 * (s / 9);
-    if (s > 0) {
-      // issued by this wave after B(s) (at step s - 1): the halo piece of step s - 1, if any.
-      // (A deeper, 3-slot B ring measured slower: 68 -> 74 us on the 64x64 320-channel conv.)
-      const int pt = tap == 0 ? 8 : tap - 1;
-      const int pcb = tap == 0 ? cb - 1 : cb;
-      if (pcb + 1 < cb1 && has_piece(pt)) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_barrier" ::: "memory");
+  // channel blocks outer, the 9 taps unrolled inside: tap-dependent offsets are compile-time indices
+  int s = 0;
+  for (int cb = cb0; cb < cb1; ++cb) {
+    const int abuf = (cb & 1) * HALO_U4 * 16;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap, ++s) {
+      if (s > 0) {
+        // issued by this wave after B(s) (at step s - 1): the halo piece of step s - 1, if any.
+        // (A deeper, 3-slot B ring measured slower: 68 -> 74 us on the 64x64 320-channel conv.)
+        const int pt = tap == 0 ? 8 : tap - 1;
+        const int pcb = tap == 0 ? cb - 1 : cb;
+        if (pcb + 1 < cb1 && has_piece(pt)) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");
+      }
+      if (s + 1 < nsteps) {
+        if (tap < 8) issue_b(cb, tap + 1, (s + 1) % NBS);
+        else issue_b(cb + 1, 0, (s + 1) % NBS);
+      }
+      if (cb + 1 < cb1 && has_piece(tap)) issue_halo(cb + 1, tap);
+      compute(tap, abuf, s % NBS);
     }
-    if (s + 1 < nsteps) issue_b(s + 1);
-    if (cb + 1 < cb1 && has_piece(tap)) issue_halo(cb + 1, tap);
-    compute(s);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
