@@ -786,14 +786,21 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(const ConvArgs p) {
 //         before step s only the halo piece issued after B(s) may stay in flight
 // ---------------------------------------------------------------------------------------
 namespace halo {
-constexpr int BN = 160, NT = 512, PIECES_PER_TAP = 8, NBS = 2;   // one 1-KB halo piece per wave per tap; 2 B slots
-constexpr int B_U4 = BN * 8;                                      // uint4 per B slot (20,480 B)
+constexpr int BN = 160, NT = 512, PIECES_PER_TAP = 8;   // one 1-KB halo piece per wave per tap
+constexpr int B_U4 = BN * 8;                            // uint4 per B slot (20,480 B)
+constexpr int DUMMY_U4 = 64;                            // 1-KB target of the count-keeping dummy DMAs
 template <int W, int R> struct Geo {
   static constexpr int HW = W + 2, HPIX = (R + 2) * HW;          // halo row pitch, halo pixels
   static constexpr int NP = (HPIX * 8 + 63) / 64;                // 1-KB pieces per halo
   static constexpr int A_TAPS = (NP + PIECES_PER_TAP - 1) / PIECES_PER_TAP;
   static constexpr int HALO_U4 = NP * 64;
-  static constexpr int SMEM_U4 = 2 * HALO_U4 + NBS * B_U4;       // W=64, R=4: 143,360 B
+  // B ring depth: as many 20-KB slots as the LDS left by the two halo buffers holds, 2..4 (W = 64:
+  // 2; W = 32, 4 rows: 4; W = 32, 8 rows and W = 16: 3).  The 32x32 / 16x16 levels stream weights
+  // that are cold in L2 in a denoising step (7-30 MB per conv), so one K step of lookahead waits out
+  // the HBM latency every step; the 64x64 level's 1.8 MB of weights stay hot
+  static constexpr int NBS_FIT = (10240 - 2 * HALO_U4 - DUMMY_U4) / B_U4;
+  static constexpr int NBS = NBS_FIT < 2 ? 2 : (NBS_FIT > 4 ? 4 : NBS_FIT);
+  static constexpr int SMEM_U4 = 2 * HALO_U4 + NBS * B_U4 + DUMMY_U4;   // W=64, R=4: 144,384 B
 };
 }  // namespace halo
 
@@ -804,6 +811,7 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
   typedef Geo<W, R> G;
   constexpr int BM = R * W;
   constexpr int HW = G::HW, HPIX = G::HPIX, NP = G::NP, A_TAPS = G::A_TAPS, HALO_U4 = G::HALO_U4;
+  constexpr int NBS = G::NBS;
   static_assert(A_TAPS <= 7, "halo geometry");
   constexpr int WT = BM / 4;                      // wave tile rows
   constexpr int FM = WT / 16, FN = 5;
@@ -879,7 +887,15 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
     hoff0[t] = ok ? (pix * p.c0 + 8 * c) * 2 : kOOB;
     hoff1[t] = ok ? (pix * (p.c1 > 0 ? p.c1 : 1) + 8 * c) * 2 : kOOB;
   }
-  auto issue_halo = [&](int cb, int tap) {
+  // Every wave issues exactly 3 B DMAs + 1 halo piece per step (OOB dummies into a 1-KB scratch
+  // where a wave has fewer), so the vmcnt that retires B(s) is one compile-time number for the
+  // NBS-deep ring: the piece issued after B(s) + (NBS - 2) later steps of 4
+  const unsigned lds_dummy = __builtin_amdgcn_readfirstlane(lds0 + (unsigned)((2 * HALO_U4 + NBS * B_U4) * 16));
+  auto issue_halo = [&](int cb, int tap, bool real) {
+    if (!real) {
+      dma16s(ra0, kOOB, 0, lds_dummy);
+      return;
+    }
     const int j = tap * PIECES_PER_TAP + wv;
     const bool src1 = p.c1 > 0 && cb * 64 >= p.c0;            // uniform per channel block
     const int soff = __builtin_amdgcn_readfirstlane((cb * 64 - (src1 ? p.c0 : 0)) * 2);
@@ -888,7 +904,7 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
     else dma16s(ra0, hoff0[tap], soff, dst);
   };
   // B tile of step (cb, tap): rows n0 + r (r < 160), packed-K columns tap * cin + cb * 64 .. + 64;
-  // waves 0-3 load rows rr, rr + 64, rr + 128 (rr < 32 for the last), waves 4-7 two
+  // waves 0-3 load rows rr, rr + 64, rr + 128 (rr < 32 for the last), waves 4-7 two (+ a dummy)
   const int rr = tid >> 3, cc = tid & 7;               // rr in [0, 64)
   const int cl = cc ^ ((rr >> 1) & 7);                 // (rr + 64 i) >> 1 & 7 == rr >> 1 & 7
   int boff[3];
@@ -897,13 +913,13 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
     const int r = rr + 64 * i, n = n0 + r;
     boff[i] = (r < BN && n < p.n) ? (n * p.kpad + 8 * cl) * 2 : kOOB;
   }
-  auto issue_b = [&](int cb, int tap, int slotb) {
+  auto issue_b = [&](int cb, int tap, int slotb, bool real) {
     const int soff = __builtin_amdgcn_readfirstlane((tap * p.cin + cb * 64) * 2);
     const unsigned base = lds_b + (unsigned)(slotb * B_U4 * 16);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      if (i == 2 && wv >= 4) break;
-      dma16s(rw, boff[i], soff, __builtin_amdgcn_readfirstlane(base + (unsigned)((64 * i + 8 * wv) * 128)));
+      if (!real || (i == 2 && wv >= 4)) dma16s(rw, kOOB, 0, lds_dummy);
+      else dma16s(rw, boff[i], soff, __builtin_amdgcn_readfirstlane(base + (unsigned)((64 * i + 8 * wv) * 128)));
     }
   };
 
@@ -953,33 +969,31 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
     }
   };
 
-  // prologue: the whole halo of channel block cb0 and B of step 0
+  // prologue: the whole halo of channel block cb0, then B(0 .. NBS - 2) as count-keeping groups
 #pragma unroll
   for (int t = 0; t < A_TAPS; ++t)
-    if (has_piece(t)) issue_halo(cb0, t);
-  issue_b(cb0, 0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+    if (has_piece(t)) issue_halo(cb0, t, true);
+#pragma unroll
+  for (int q = 0; q < NBS - 1; ++q) {
+    issue_b(cb0 + q / 9, q % 9, q, q < nsteps);
+    issue_halo(cb0, 0, false);
+  }
   // channel blocks outer, the 9 taps unrolled inside: tap-dependent offsets are compile-time indices
   int s = 0;
   for (int cb = cb0; cb < cb1; ++cb) {
     const int abuf = (cb & 1) * HALO_U4 * 16;
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap, ++s) {
-      if (s > 0) {
-        // issued by this wave after B(s) (at step s - 1): the halo piece of step s - 1, if any.
-        // (A deeper, 3-slot B ring measured slower: 68 -> 74 us on the 64x64 320-channel conv.)
-        const int pt = tap == 0 ? 8 : tap - 1;
-        const int pcb = tap == 0 ? cb - 1 : cb;
-        if (pcb + 1 < cb1 && has_piece(pt)) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_barrier" ::: "memory");
+      // B(s) has landed for this wave: younger and allowed in flight are the piece issued after it
+      // and the NBS - 2 later steps' groups; then every wave's part of B(s) (and, at tap 0, of the
+      // channel block's halo) is in LDS, and every wave is done with step s - 1's B slot
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(1 + 4 * (NBS - 2)) : "memory");
+      asm volatile("s_barrier" ::: "memory");
+      {
+        const int NT_ = (tap + NBS - 1) % 9, NC_ = (tap + NBS - 1) / 9;
+        issue_b(cb + NC_, NT_, (s + NBS - 1) % NBS, s + NBS - 1 < nsteps);
       }
-      if (s + 1 < nsteps) {
-        if (tap < 8) issue_b(cb, tap + 1, (s + 1) % NBS);
-        else issue_b(cb + 1, 0, (s + 1) % NBS);
-      }
-      if (cb + 1 < cb1 && has_piece(tap)) issue_halo(cb + 1, tap);
+      issue_halo(cb + 1, tap, cb + 1 < cb1 && has_piece(tap));
       compute(tap, abuf, s % NBS);
     }
   }
