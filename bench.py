@@ -93,7 +93,9 @@ def roofline(unet, stepper, ts, nsteps, dtype, fp8=False):
     peak_tf = PEAK_BF16_TFLOPS if dtype == torch.bfloat16 else PEAK_FP32_TFLOPS
     per_step = {}
     for k, v in fam.items():
-        e = dict(launches=v["launches"] // nsteps, ms=round(v["ms"] / nsteps, 4),
+        # eager_event_ms: HIP events around every launch of eager (non-graph) steps — it carries ~5-7 us of
+        # dispatch per launch, so the families sum to more than the graph-replayed ms_per_step
+        e = dict(launches=v["launches"] // nsteps, eager_event_ms=round(v["ms"] / nsteps, 4),
                  gflop=round(v["flops"] / nsteps / 1e9, 2), mb=round(v["bytes"] / nsteps / 1e6, 2))
         sec = v["ms"] * 1e-3
         if v["flops"] > 0:      # MFMA-bound family: fraction of the dense MFMA peak
@@ -204,7 +206,9 @@ def main():
     ap.add_argument("--latent", default="64", help="latent side L (LxL) or HxW, e.g. 32x64 for config 5's 256x512 frames")
     ap.add_argument("--fp8", action="store_true",
                     help="config 5: self-attention on the fp8 (e4m3) MFMA path (UNet.set_attention_fp8)")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
+                    help="compute dtype (default: bf16, the reference's fp16-autocast width; --mode ae: fp32, config "
+                         "1's reference precision, trainers_ae.py:279-389)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-steps", type=int, default=2)
@@ -217,6 +221,8 @@ def main():
     ap.add_argument("--zero", action="store_true",
                     help="train mode: ZeRO-1 sharded AdamW (train_diffusion.sh:27 optimizer_zero_redundancy)")
     args = ap.parse_args()
+    if args.dtype is None:
+        args.dtype = "fp32" if args.mode == "ae" else "bf16"
     if args.mode == "train":
         return main_train(args)
     if args.mode == "sample":

@@ -49,6 +49,10 @@ constexpr int SCR_F = 2048;
 // instruction, into a dummy LDS row per wave) while K tile s + 1 streams, so the DMA of every K tile
 // finds its lines in the XCD's L2 instead of waiting on Infinity-Cache / HBM latency
 constexpr int PF_INS = 2;                   // per wave: 72 of the 576 lines
+#ifndef WIDE_PFD
+#define WIDE_PFD 2
+#endif
+constexpr int PFD = WIDE_PFD;               // K tiles ahead of the one being multiplied that are touched
 constexpr int PF_BYTES = 64 * 8;            // dummy LDS: 64 B per wave
 constexpr int SCR_C1 = 512, SCR_ROW = 1024;
 constexpr int NST = FM * FN / 2;            // epilogue store instructions per lane (20)
@@ -228,7 +232,9 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
   };
 
   if (total > 0) issue(0);
-  if (total > 1) prefetch(1);
+#pragma unroll
+  for (int q = 1; q < PFD; ++q)
+    if (total > q) prefetch(q);
   int s = 0;
   for (int r = 0; r < my_tiles; ++r) {
     int m0, n0;
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
     for (int kt = 0; kt < nks; ++kt, ++s) {
       // K tile s landed for this wave; younger and allowed to stay in flight: the prefetch of K tile
       // s + 1 (issued right after this tile's DMA) and, after an epilogue, its NST stores
-      const bool pf = s + 1 < total, epi = kt == 0 && r > 0;
+      const bool pf = s + PFD - 1 < total, epi = kt == 0 && r > 0;
       if (pf && epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PF_INS + NST) : "memory");
       else if (epi) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
       else if (pf) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PF_INS) : "memory");
@@ -248,7 +254,7 @@ __global__ __launch_bounds__(512, 2) void gemm_wide_kernel(const ConvArgs p) {
       // every wave's part of tile s is in LDS, and every wave is done with slot (s + 1) & 1
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       if (s + 1 < total) issue(s + 1);
-      if (s + 2 < total) prefetch(s + 2);
+      if (s + PFD < total) prefetch(s + PFD);
       compute(s & 1);
     }
     // ---- epilogue from registers; this tile's scratch landed with its second K tile
