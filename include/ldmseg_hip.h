@@ -147,9 +147,13 @@ void ldm_conv2d_set_wide(int mode);
 /* Tuning hook: the deep-ring 1x1 GEMM of the 16x16 / 8x8 levels (csrc/gemm_ring.hip): 0 planner, 1 never,
    2 whenever legal. */
 void ldm_conv2d_set_ring(int mode);
-/* Tuning hook: column width of the split-K reduction kernel's 64-row tiles — 0 = planner's choice
+/* Tuning hook: column width of the split-K reduction kernel's tiles — 0 = planner's choice
  * (64 when 128-wide tiles give fewer than 512 blocks), 64 or 128 forced. */
 void ldm_conv2d_set_splitk_cols(int cols);
+/* Tuning hook: row count of the split-K reduction kernel's tiles — 0 = planner's choice (64, halved
+ * down to 16 while the 64-column tiles give fewer than 512 blocks), 16, 32 or 64 forced (16 with
+ * 128 columns runs 32). */
+void ldm_conv2d_set_splitk_rows(int rows);
 /* Tuning hook: bf16 NHWC epilogue of the 2-blocks-per-CU tiles — 0 = bias / time embedding /
  * activation applied from the accumulators and the tile staged once as bf16 (default),
  * 1 = fp32 staging in row halves (the round-1 form). */

@@ -466,22 +466,27 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   }
 }
 
-// Split-K reduction + full epilogue: one block per 64-row x COLS-channel tile (COLS 64 when
-// 128-wide tiles would leave the chip under-filled: the 8x8 / 16x16 levels have 80-320 of
-// them).  Per thread the loads of two splits are in flight before their adds.
-template <typename T, int COLS = 128>
+// Split-K reduction + full epilogue: one block per ROWS x COLS tile (COLS 64 when 128-wide tiles
+// would leave the chip under-filled: the 8x8 / 16x16 levels have 80-320 of them; ROWS 32 / 16 when
+// even 64-row tiles give < 512 blocks: config 2's single frame, where a 64-row block's slab loads
+// formed a chain of dependent rounds on 20-320 CUs).  Per thread the loads of up to 16 / NQ splits
+// are in flight before their adds; the splits are summed in index order (every tile shape gives the
+// same bits).
+template <typename T, int COLS = 128, int ROWS = 64>
 __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) {
-  constexpr int ROWS = 64, PITCH = COLS + 4, RPQ = 256 / (COLS / 4);   // 8 or 16 rows per pass
+  constexpr int PITCH = COLS + 4, RPQ = 256 / (COLS / 4);   // 8 or 16 rows per pass
+  static_assert(ROWS % RPQ == 0, "tile rows");
   constexpr int NQ = ROWS / RPQ;
+  constexpr int G = 16 / NQ > 4 ? 16 / NQ : 4;                // splits whose loads are in flight together
   constexpr int RED = gn_red_floats<256, COLS, ROWS, 8>() > gn_red_floats<256, COLS, ROWS, 4>()
                           ? gn_red_floats<256, COLS, ROWS, 8>() : gn_red_floats<256, COLS, ROWS, 4>();
   constexpr int SF = ROWS * PITCH > RED ? ROWS * PITCH : RED;
   __shared__ float stage[SF];   // also the statistics scratch of either epilogue
   const int tiles_n = (p.n + COLS - 1) / COLS;
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
-  const int m0 = tm * 64, n0 = tn * COLS;
+  const int m0 = tm * ROWS, n0 = tn * COLS;
   const int64_t slab = (int64_t)p.M * p.n;
-  // phase A: sum the slabs into LDS; the rows of a thread for two splits are loaded together
+  // phase A: sum the slabs into LDS
   {
     const int c4 = threadIdx.x % (COLS / 4), r0 = threadIdx.x / (COLS / 4);
     const int n = n0 + 4 * c4;
@@ -507,35 +512,40 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) 
         }
       }
     };
+    auto add = [&](const float4* x) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        acc[q].x += x[q].x; acc[q].y += x[q].y; acc[q].z += x[q].z; acc[q].w += x[q].w;
+      }
+    };
     int sp = 0;
-    for (; sp + 3 < p.ksplit; sp += 4) {
-      float4 x[4][NQ];
+    for (; sp + G - 1 < p.ksplit; sp += G) {
+      float4 x[G][NQ];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) load(sp + u, x[u]);
+      for (int u = 0; u < G; ++u) load(sp + u, x[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < G; ++u) add(x[u]);
+    }
+    if constexpr (G > 4) {
+      for (; sp + 3 < p.ksplit; sp += 4) {
+        float4 x[4][NQ];
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          acc[q].x += x[u][q].x; acc[q].y += x[u][q].y; acc[q].z += x[u][q].z; acc[q].w += x[u][q].w;
-        }
+        for (int u = 0; u < 4; ++u) load(sp + u, x[u]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) add(x[u]);
+      }
     }
     for (; sp + 1 < p.ksplit; sp += 2) {
       float4 x[NQ], y[NQ];
       load(sp, x);
       load(sp + 1, y);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        acc[q].x += x[q].x; acc[q].y += x[q].y; acc[q].z += x[q].z; acc[q].w += x[q].w;
-        acc[q].x += y[q].x; acc[q].y += y[q].y; acc[q].z += y[q].z; acc[q].w += y[q].w;
-      }
+      add(x);
+      add(y);
     }
     if (sp < p.ksplit) {
       float4 x[NQ];
       load(sp, x);
-#pragma unroll
-      for (int q = 0; q < NQ; ++q) {
-        acc[q].x += x[q].x; acc[q].y += x[q].y; acc[q].z += x[q].z; acc[q].w += x[q].w;
-      }
+      add(x);
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q)
@@ -1078,14 +1088,30 @@ int launch_halo(ConvArgs a, hipStream_t s) {
 }
 
 int g_splitk_cols = 0;    // tuning hook (ldm_conv2d_set_splitk_cols): 0 planner, 64 / 128 forced
+int g_splitk_rows = 0;    // tuning hook (ldm_conv2d_set_splitk_rows): 0 planner, 16 / 32 / 64 forced
+
+// The reduction's tile: 64 x 128 while that gives >= 512 blocks, else 64 columns, and rows halved
+// (64 -> 32 -> 16) until >= 512 blocks (config 2's single frame: the 8x8 level's M = 64 x 1280
+// reduction had 20 64x64 blocks)
+void splitk_tile(int M, int n, int* rows, int* cols) {
+  auto blocks = [&](int r, int c) { return ((M + r - 1) / r) * ((n + c - 1) / c); };
+  *cols = g_splitk_cols ? g_splitk_cols : (blocks(64, 128) >= 512 ? 128 : 64);
+  if (g_splitk_rows) { *rows = *cols == 128 && g_splitk_rows == 16 ? 32 : g_splitk_rows; return; }
+  *rows = 64;
+  if (*cols == 64)
+    while (*rows > 16 && blocks(*rows, 64) < 512) *rows >>= 1;
+}
 
 template <typename T>
 void launch_splitk_epilogue(const ConvArgs& a, hipStream_t s) {
-  const int mt = (a.M + 63) / 64;
-  const int b128 = mt * ((a.n + 127) / 128);
-  const bool narrow = g_splitk_cols == 64 || (g_splitk_cols == 0 && b128 < 512);
-  if (narrow) hipLaunchKernelGGL((splitk_epilogue_kernel<T, 64>), dim3(mt * ((a.n + 63) / 64)), dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((splitk_epilogue_kernel<T, 128>), dim3(b128), dim3(256), 0, s, a);
+  int rows, cols;
+  splitk_tile(a.M, a.n, &rows, &cols);
+  const dim3 grid(((a.M + rows - 1) / rows) * ((a.n + cols - 1) / cols));
+  if (cols == 128 && rows == 32) hipLaunchKernelGGL((splitk_epilogue_kernel<T, 128, 32>), grid, dim3(256), 0, s, a);
+  else if (cols == 128) hipLaunchKernelGGL((splitk_epilogue_kernel<T, 128, 64>), grid, dim3(256), 0, s, a);
+  else if (rows == 16) hipLaunchKernelGGL((splitk_epilogue_kernel<T, 64, 16>), grid, dim3(256), 0, s, a);
+  else if (rows == 32) hipLaunchKernelGGL((splitk_epilogue_kernel<T, 64, 32>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((splitk_epilogue_kernel<T, 64, 64>), grid, dim3(256), 0, s, a);
 }
 
 int g_force_stages = 0;   // tuning hook: 1 register-staged operands, 3 / 4 ring depth, 0 planner
@@ -1434,6 +1460,9 @@ extern "C" void ldm_conv2d_set_halo_split(int ks) { g_halo_split = ks > 0 ? ks :
 extern "C" void ldm_conv2d_set_halo_rows32(int rows) { g_halo32_rows = (rows == 4 || rows == 8) ? rows : 0; }
 extern "C" void ldm_conv2d_set_ars(int mode) { g_ars_mode = (mode >= 1 && mode <= 3) ? mode : 0; }
 extern "C" void ldm_conv2d_set_splitk_cols(int cols) { g_splitk_cols = (cols == 64 || cols == 128) ? cols : 0; }
+extern "C" void ldm_conv2d_set_splitk_rows(int rows) {
+  g_splitk_rows = (rows == 16 || rows == 32 || rows == 64) ? rows : 0;
+}
 extern "C" void ldm_conv2d_set_epilogue(int mode) { g_epi_pre = mode == 1 ? 0 : 1; }
 extern "C" void ldm_conv2d_force_stages(int stages) {
   g_force_stages = (stages == 1 || stages == 3 || stages == 4) ? stages : 0;   // 1: register-staged operands

@@ -87,6 +87,7 @@ EXPORTS = {
     "ldm_conv2d_set_wide": (None, [_i]),
     "ldm_conv2d_set_ring": (None, [_i]),
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
+    "ldm_conv2d_set_splitk_rows": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_feedforward": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
     "ldm_transformer_in": (_i, [ctypes.POINTER(GnFold), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
@@ -715,6 +716,11 @@ def set_conv_ring(mode=0):
 def set_conv_splitk_cols(cols=0):
     """Tuning hook: split-K reduction tile width — 0 planner, 64 or 128 forced."""
     load_library().ldm_conv2d_set_splitk_cols(int(cols))
+
+
+def set_conv_splitk_rows(rows=0):
+    """Tuning hook: split-K reduction tile rows — 0 planner, 16, 32 or 64 forced."""
+    load_library().ldm_conv2d_set_splitk_rows(int(rows))
 
 
 def set_conv_epilogue(mode=0):
