@@ -340,6 +340,34 @@ def test_attention_d40_qs2_close_to_default(B, N):
     assert torch.equal(outs[0], outs[2])
 
 
+@pytest.mark.parametrize("B,N,hd", [(4, 4096, 40), (4, 4096 + 37, 40), (4, 64 * 3 + 5, 40), (4, 64, 40), (4, 40, 40),
+                                    (8, 1024, 80), (8, 1024 + 19, 80)])
+def test_attention_skew_bit_identical(B, N, hd):
+    """ldm_attention_set_skew(2): the 32x32x16 head_dim 40 / 80 kernel with the block's upper waves one
+    half-iteration behind (softmax + P.V of tile t - 1 before Q.K^T of tile t).  Every wave runs the
+    same operations in the same order, so output and log-sum-exp are bit-identical to the default
+    form; N covers 0, 1, 3 and 64 full key tiles plus ragged tails."""
+    torch.manual_seed(10)
+    C, H = 8 * hd, 8
+    qkv = torch.randn(B, N, 3 * C, device=DEV).to(torch.bfloat16)
+    outs = []
+    try:
+        if hd == 40:
+            K.set_attention_waves(8)        # the 8-wave two-blocks-per-CU kernel at every N
+        for mode in (1, 2):
+            K.set_attention_skew(mode)
+            o, lse = K.attention_fwd_lse(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C, 3 * C)
+            outs.append((o, lse))
+    finally:
+        K.set_attention_skew(0)
+        K.set_attention_waves(0)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    x = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(x[0] @ x[1].transpose(-1, -2) * hd ** -0.5, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B, N, C)
+    assert ((outs[1][0].float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
 def test_attention_softmax_spike():
     """Force the online-softmax rescale: a huge logit in the LAST kv tile of some rows."""
     torch.manual_seed(4)

@@ -50,12 +50,13 @@ def mm_case(M, K, N):
     return (lambda: torch.mm(a, b)), 2.0 * M * K * N, None
 
 
-def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True, d80=True, qs2=0):
+def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True, d80=True, qs2=0, skew=0):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
     def run():
         K.set_attention_d80(d80)
         K.set_attention_qs2(qs2)
+        K.set_attention_skew(skew)
         K.force_attention_legacy(legacy)
         K.set_attention_waves(waves)
         K.set_attention_maxcol(maxcol)
@@ -291,6 +292,12 @@ CASES = {
     "conv3_upsample_l3": lambda: conv_case(8, 8, 8, 1280, 1280, up=True, stats=True),
     "conv3_upsample_l3_ph": lambda: conv_case(8, 8, 8, 1280, 1280, up=True, stats=True, phases=True),
     "conv3_l2_up_2560": lambda: conv_case(8, 16, 16, 2560, 1280, c1=1280, residual=True, stats=True),
+    "gemm_short_l1_1920": lambda: conv_case(8, 32, 32, 1920, 640, k=1, c1=640, residual=True),
+    "gemm_short_l1_1280": lambda: conv_case(8, 32, 32, 1280, 640, k=1, c1=640, residual=True),
+    "gemm_short_l1_960": lambda: conv_case(8, 32, 32, 960, 640, k=1, c1=320, residual=True),
+    "gemm_short_l1_in": lambda: conv_case(8, 32, 32, 320, 640, k=1, residual=True),
+    "gemm_short_l0_960": lambda: conv_case(8, 64, 64, 960, 320, k=1, c1=320, residual=True),
+    "gemm_short_l0_640": lambda: conv_case(8, 64, 64, 640, 320, k=1, c1=320, residual=True),
     "gemm_proj_1280_l2": lambda: conv_case(8, 16, 16, 1280, 1280, k=1, residual=True),
     "gemm_proj_1280_l3": lambda: conv_case(8, 8, 8, 1280, 1280, k=1, residual=True),
     "gemm_short_l3_2560": lambda: conv_case(8, 8, 8, 2560, 1280, k=1, c1=1280, residual=True),
@@ -344,6 +351,12 @@ CASES = {
     "attn_c5_2048_d40_fp8pv": lambda: attn_case(16, 2048, 320, fp8=True, scaled=False),
     "attn_4096_d40_fp8": lambda: attn_case(8, 4096, 320, fp8=True),
     "attn_4096_d40_qs2": lambda: attn_case(8, 4096, 320, qs2=1),
+    "attn_4096_d40_noskew": lambda: attn_case(8, 4096, 320, skew=1),
+    "attn_4096_d40_skew": lambda: attn_case(8, 4096, 320, skew=2),
+    "attn_1024_d80_noskew": lambda: attn_case(8, 1024, 640, skew=1),
+    "attn_1024_d80_skew": lambda: attn_case(8, 1024, 640, skew=2),
+    "attn_c5_2048_d40_noskew": lambda: attn_case(16, 2048, 320, skew=1),
+    "attn_c5_2048_d40_skew": lambda: attn_case(16, 2048, 320, skew=2),
     "attn_4096_d40_pipe": lambda: attn_case(8, 4096, 320, qs2=2),
     "attn_c5_2048_d40_qs2": lambda: attn_case(16, 2048, 320, qs2=1),
     "attn_c5_2048_d40_pipe": lambda: attn_case(16, 2048, 320, qs2=2),

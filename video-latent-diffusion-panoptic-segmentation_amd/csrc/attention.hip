@@ -682,8 +682,15 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 // level).  Q.K^T runs over DQ = D + 1 (the max column) rounded up to 16 (48 / 96: 3 / 6 MFMAs per
 // 32-key block), P.V over ND32 = ceil((D + 1) / 32) 32-row head-dim blocks (2 / 3, the ones column
 // d = D carrying the denominator).
-template <int NW, int OCC, int KT = 64, int D = 40, int QS = 1>
-__global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p) {
+// SKEW: the block's waves in two phases one half-iteration apart, so the two waves of a block on a
+// SIMD (waves w and w + 4) do not want the matrix pipe and the VALU at the same time: the upper half
+// ("lagging" waves) run the softmax and P.V of tile t - 1 and then Q.K^T of tile t between the same
+// barriers in which the lower half run Q.K^T, softmax and P.V of tile t.  Per wave the operations
+// and their order are unchanged (bit-identical); V of tile t - 1 stays readable, so three K/V buffers.
+// (__launch_bounds__' second argument is waves per SIMD: OCC blocks of NW waves need OCC * NW / 4; the
+// default form meets it at 127 VGPRs unasked, the SKEW form is held to it)
+template <int NW, int OCC, int KT = 64, int D = 40, int QS = 1, bool SKEW = false>
+__global__ __launch_bounds__(64 * NW, SKEW ? OCC * NW / 4 : OCC) void attn_d40_kernel(const AttnArgs p) {
   typedef bf16_t T;
   typedef __attribute__((ext_vector_type(16))) float f32x16_t;
   static_assert(D % 8 == 0, "head dim");
@@ -691,7 +698,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   constexpr int DQ = (D + 16) / 16 * 16, QC = DQ / 16, ND32 = (D + 32) / 32;
   constexpr int EPC = 8, CPR = (DQ > 32 * ND32 ? DQ : 32 * ND32) / 8, RCH = CPR + 1, ROW = RCH * EPC,
                 TILE = KT * ROW, ES = 2;
-  __shared__ uint4 smem[2 * 2 * TILE * ES / 16];
+  constexpr int NB = SKEW ? 3 : 2;                  // K/V tile buffers
+  __shared__ uint4 smem[NB * 2 * TILE * ES / 16];
   T* const lds = reinterpret_cast<T*>(smem);
   typedef __attribute__((address_space(3))) uint4 lds_u4_t;
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_u4_t*)smem;
@@ -829,13 +837,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
                                  pack_bf16x2(pv[6], pv[7]));
       }
   };
-  auto compute = [&](int buf, int kv0, bool masked, bool first, int half) {
+  // S^T = K Q^T of one 64-key half of the tile in buffer buf: each K fragment read from LDS feeds the
+  // MFMAs of every subtile
+  auto qk = [&](int buf, int half, f32x16_t (&sacc)[QS][2]) {
     const T* Ks = lds + buf * 2 * TILE + half * 64 * ROW;
-    const T* Vs = lds + buf * 2 * TILE + TILE + half * 64 * ROW;
-    kv0 += 64 * half;
-    first = first && half == 0;
-    f32x16_t sacc[QS][2];
-    // S^T = K Q^T: each K fragment read from LDS feeds the MFMAs of every subtile
 #pragma unroll
     for (int blk = 0; blk < 2; ++blk) {
 #pragma unroll
@@ -852,15 +857,11 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
                                                                  __builtin_bit_cast(bf16x8_t, qf[s][c]), sacc[s][blk], 0, 0, 0);
       }
     }
-    if (masked) {
-#pragma unroll
-      for (int s = 0; s < QS; ++s)
-#pragma unroll
-        for (int blk = 0; blk < 2; ++blk)
-#pragma unroll
-          for (int r = 0; r < 16; ++r)
-            if (kv0 + 32 * blk + 8 * (r >> 2) + 4 * hh + (r & 3) >= p.nkv) sacc[s][blk][r] = -INFINITY;
-    }
+  };
+  // the online softmax of S^T (running max, lazy rescale, P = exp2) and O^T += V^T P^T for the same
+  // half of the tile in buffer buf
+  auto smpv = [&](f32x16_t (&sacc)[QS][2], int buf, int half, bool first) {
+    const T* Vs = lds + buf * 2 * TILE + TILE + half * 64 * ROW;
     float mx[QS];
     bool resc = first;
 #pragma unroll
@@ -908,22 +909,67 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
         }
     }
   };
+  auto compute = [&](int buf, int kv0, bool masked, bool first, int half) {
+    f32x16_t sacc[QS][2];
+    qk(buf, half, sacc);
+    kv0 += 64 * half;
+    if (masked) {
+#pragma unroll
+      for (int s = 0; s < QS; ++s)
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * blk + 8 * (r >> 2) + 4 * hh + (r & 3) >= p.nkv) sacc[s][blk][r] = -INFINITY;
+    }
+    smpv(sacc, buf, half, first && half == 0);
+  };
 
   const int ntiles = (p.nkv + KT - 1) / KT;
   const int nfull = p.nkv / KT;
+  auto bufi = [](int t) { return NB == 3 ? t % 3 : t & 1; };
+  auto issue_next = [&](int t) {   // tile t + 1 while tile t is multiplied
+    if (t + 1 < nfull) issue_full(bufi(t + 1));
+    else if (t + 1 < ntiles) issue_tile((t + 1) * KT, bufi(t + 1));
+  };
   issue_tile(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int t = 0; t < nfull; ++t) {
-    if (t + 1 < nfull) issue_full((t + 1) & 1);
-    else if (t + 1 < ntiles) issue_tile((t + 1) * KT, (t + 1) & 1);
+  if constexpr (!SKEW) {
+    for (int t = 0; t < nfull; ++t) {
+      issue_next(t);
 #pragma unroll
-    for (int hf = 0; hf < KT / 64; ++hf) compute(t & 1, t * KT, false, t == 0, hf);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+      for (int hf = 0; hf < KT / 64; ++hf) compute(bufi(t), t * KT, false, t == 0, hf);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    // one loop for both phases: S^T of the lagging waves stays in sp across the barrier
+    const bool lag = __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
+    f32x16_t sp[KT / 64][QS][2];
+    for (int t = 0; t < nfull; ++t) {
+      issue_next(t);
+      if (lag && t > 0) {
+#pragma unroll
+        for (int hf = 0; hf < KT / 64; ++hf) smpv(sp[hf], bufi(t - 1), hf, t == 1 && hf == 0);
+      }
+#pragma unroll
+      for (int hf = 0; hf < KT / 64; ++hf) qk(bufi(t), hf, sp[hf]);
+      if (!lag) {
+#pragma unroll
+        for (int hf = 0; hf < KT / 64; ++hf) smpv(sp[hf], bufi(t), hf, t == 0 && hf == 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (lag && nfull > 0) {
+#pragma unroll
+      for (int hf = 0; hf < KT / 64; ++hf) smpv(sp[hf], bufi(nfull - 1), hf, nfull == 1 && hf == 0);
+    }
   }
   if (nfull < ntiles) {
-    for (int hf = 0; hf < KT / 64 && nfull * KT + 64 * hf < p.nkv; ++hf) compute(nfull & 1, nfull * KT, true, nfull == 0, hf);
+    for (int hf = 0; hf < KT / 64 && nfull * KT + 64 * hf < p.nkv; ++hf)
+      compute(bufi(nfull), nfull * KT, true, nfull == 0, hf);
   }
 
   // denominator: O^T row d = D = block D / 32, register 4 ((D % 32) / 8) of the hh = 0 lane of this
@@ -1268,6 +1314,7 @@ int launch32_dp_mc(const AttnArgs& a, int batch, hipStream_t s) {
 }
 
 int g_attn_d80 = 1;      // tuning / A-B hook: 0 routes head_dim 80 to the 16x16x32 kernel
+int g_attn_skew = 0;     // tuning / A-B hook (ldm_attention_set_skew): 0 planner, 1 off, 2 on
 int g_attn_qs2 = 0;      // tuning / A-B hook: head_dim 40 as 64 queries per wave: 1 two subtiles in step,
                          // 2 the pipelined form (attn_d40p_kernel)
 
@@ -1277,7 +1324,9 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
     if (!F8 && g_attn_d80 && a.d == 80) {
       // the 32x32x16 form at head_dim 80 (the 32x32 level): 8 waves x 32 queries per block
       const int nb8 = (a.nq + 255) / 256 * a.heads * batch;
-      if (nb8 >= 256) hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80>), dim3(nb8), dim3(512), 0, s, a);
+      if (nb8 >= 256 && g_attn_skew == 2)
+        hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80, 1, true>), dim3(nb8), dim3(512), 0, s, a);
+      else if (nb8 >= 256) hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80>), dim3(nb8), dim3(512), 0, s, a);
       else hipLaunchKernelGGL((attn_d40_kernel<4, 2, 64, 80>), dim3((a.nq + 127) / 128 * a.heads * batch),
                               dim3(256), 0, s, a);
       LDM_CHECK_LAUNCH();
@@ -1302,6 +1351,8 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
       } else if (g_attn_waves == 4) {
         const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
         hipLaunchKernelGGL((attn_d40_kernel<4, 4>), dim3(nb4), dim3(256), 0, s, a);
+      } else if ((nblk >= 512 || g_attn_waves == 8) && g_attn_skew == 2) {
+        hipLaunchKernelGGL((attn_d40_kernel<8, 2, 64, 40, 1, true>), dim3(nblk), dim3(512), 0, s, a);
       } else if (nblk >= 512 || g_attn_waves == 8) hipLaunchKernelGGL((attn_d40_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a);
       else {
         const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
@@ -2519,6 +2570,7 @@ extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
 extern "C" void ldm_attention_set_d80(int enabled) { g_attn_d80 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_qs2(int mode) { g_attn_qs2 = mode == 1 || mode == 2 ? mode : 0; }
+extern "C" void ldm_attention_set_skew(int mode) { g_attn_skew = mode == 1 || mode == 2 ? mode : 0; }
 extern "C" void ldm_attention_set_bwd32(int enabled) { g_attn_bwd32 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_maxcol(int mode) {
   g_attn_maxcol = mode >= 1 ? 1 : 0;     // 0: per-score FMA, 16x16x32 kernel

@@ -115,6 +115,7 @@ EXPORTS = {
     "ldm_attention_force_legacy": (None, [_i]),
     "ldm_attention_set_d80": (None, [_i]),
     "ldm_attention_set_qs2": (None, [_i]),
+    "ldm_attention_set_skew": (None, [_i]),
     "ldm_attention_set_bwd32": (None, [_i]),
     "ldm_conv2d_wgrad_set_ring": (None, [_i]),
     "ldm_conv2d_wgrad_set_fast_loader": (None, [_i]),
@@ -662,6 +663,12 @@ def set_attention_qs2(mode=1):
     blocks per CU); 1 two 32-query subtiles per wave sharing each K / V fragment read (one block per
     CU); 2 the tile loop software-pipelined inside each wave (attn_d40p_kernel)."""
     load_library().ldm_attention_set_qs2(int(mode))
+
+
+def set_attention_skew(mode=0):
+    """Tuning / A-B hook for head_dim 40 / 80 on the 32x32x16 kernel: 0 planner, 1 off, 2 the block's
+    waves in two phases half an iteration apart (bit-identical)."""
+    load_library().ldm_attention_set_skew(int(mode))
 
 
 def force_attention_legacy(legacy=True):
