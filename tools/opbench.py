@@ -353,6 +353,7 @@ CASES = {
     "attn_4096_d40_qs2": lambda: attn_case(8, 4096, 320, qs2=1),
     "attn_4096_d40_noskew": lambda: attn_case(8, 4096, 320, skew=1),
     "attn_4096_d40_skew": lambda: attn_case(8, 4096, 320, skew=2),
+    "attn_4096_d40_occ1": lambda: attn_case(8, 4096, 320, skew=3),
     "attn_1024_d80_noskew": lambda: attn_case(8, 1024, 640, skew=1),
     "attn_1024_d80_skew": lambda: attn_case(8, 1024, 640, skew=2),
     "attn_c5_2048_d40_noskew": lambda: attn_case(16, 2048, 320, skew=1),

@@ -690,7 +690,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 // (__launch_bounds__' second argument is waves per SIMD: OCC blocks of NW waves need OCC * NW / 4; the
 // default form meets it at 127 VGPRs unasked, the SKEW form is held to it)
 template <int NW, int OCC, int KT = 64, int D = 40, int QS = 1, bool SKEW = false>
-__global__ __launch_bounds__(64 * NW, SKEW ? OCC * NW / 4 : OCC) void attn_d40_kernel(const AttnArgs p) {
+__global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p) {
   typedef bf16_t T;
   typedef __attribute__((ext_vector_type(16))) float f32x16_t;
   static_assert(D % 8 == 0, "head dim");
@@ -944,27 +944,34 @@ __global__ __launch_bounds__(64 * NW, SKEW ? OCC * NW / 4 : OCC) void attn_d40_k
       __syncthreads();
     }
   } else {
-    // one loop for both phases: S^T of the lagging waves stays in sp across the barrier
     const bool lag = __builtin_amdgcn_readfirstlane(wave) >= NW / 2;
-    f32x16_t sp[KT / 64][QS][2];
-    for (int t = 0; t < nfull; ++t) {
-      issue_next(t);
-      if (lag && t > 0) {
+    if (!lag) {
+      for (int t = 0; t < nfull; ++t) {
+        issue_next(t);
 #pragma unroll
-        for (int hf = 0; hf < KT / 64; ++hf) smpv(sp[hf], bufi(t - 1), hf, t == 1 && hf == 0);
+        for (int hf = 0; hf < KT / 64; ++hf) compute(bufi(t), t * KT, false, t == 0, hf);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
       }
+    } else {
+      // S^T of tile t - 1 stays in sp across the barrier
+      f32x16_t sp[KT / 64][QS][2];
+      for (int t = 0; t < nfull; ++t) {
+        issue_next(t);
+        if (t > 0) {
 #pragma unroll
-      for (int hf = 0; hf < KT / 64; ++hf) qk(bufi(t), hf, sp[hf]);
-      if (!lag) {
+          for (int hf = 0; hf < KT / 64; ++hf) smpv(sp[hf], bufi(t - 1), hf, t == 1 && hf == 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);   // tile t's S^T is not started under tile t - 1's P.V
 #pragma unroll
-        for (int hf = 0; hf < KT / 64; ++hf) smpv(sp[hf], bufi(t), hf, t == 0 && hf == 0);
+        for (int hf = 0; hf < KT / 64; ++hf) qk(bufi(t), hf, sp[hf]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    if (lag && nfull > 0) {
+      if (nfull > 0) {
 #pragma unroll
-      for (int hf = 0; hf < KT / 64; ++hf) smpv(sp[hf], bufi(nfull - 1), hf, nfull == 1 && hf == 0);
+        for (int hf = 0; hf < KT / 64; ++hf) smpv(sp[hf], bufi(nfull - 1), hf, nfull == 1 && hf == 0);
+      }
     }
   }
   if (nfull < ntiles) {
@@ -1353,6 +1360,9 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
         hipLaunchKernelGGL((attn_d40_kernel<4, 4>), dim3(nb4), dim3(256), 0, s, a);
       } else if ((nblk >= 512 || g_attn_waves == 8) && g_attn_skew == 2) {
         hipLaunchKernelGGL((attn_d40_kernel<8, 2, 64, 40, 1, true>), dim3(nblk), dim3(512), 0, s, a);
+      } else if ((nblk >= 512 || g_attn_waves == 8) && g_attn_skew == 3) {
+        // A/B reference for the skewed form: the default kernel held to one block per CU (dynamic LDS pad)
+        hipLaunchKernelGGL((attn_d40_kernel<8, 2>), dim3(nblk), dim3(512), 96 * 1024, s, a);
       } else if (nblk >= 512 || g_attn_waves == 8) hipLaunchKernelGGL((attn_d40_kernel<8, 2>), dim3(nblk), dim3(512), 0, s, a);
       else {
         const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
@@ -2570,7 +2580,7 @@ extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
 extern "C" void ldm_attention_set_d80(int enabled) { g_attn_d80 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_qs2(int mode) { g_attn_qs2 = mode == 1 || mode == 2 ? mode : 0; }
-extern "C" void ldm_attention_set_skew(int mode) { g_attn_skew = mode == 1 || mode == 2 ? mode : 0; }
+extern "C" void ldm_attention_set_skew(int mode) { g_attn_skew = mode >= 1 && mode <= 3 ? mode : 0; }
 extern "C" void ldm_attention_set_bwd32(int enabled) { g_attn_bwd32 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_maxcol(int mode) {
   g_attn_maxcol = mode >= 1 ? 1 : 0;     // 0: per-score FMA, 16x16x32 kernel
