@@ -248,7 +248,8 @@ void ldm_attention_set_d80(int enabled);
 void ldm_attention_set_qs2(int enabled);
 /* Tuning / A-B hook: the head_dim 40 / 80 kernels with the block's waves in two phases half an
  * iteration apart (the upper half runs softmax + P.V of tile t - 1, then Q.K^T of tile t, beside the
- * lower half's tile t; three K/V buffers; bit-identical): 0 = planner's choice, 1 = off, 2 = on. */
+ * lower half's tile t; three K/V buffers; bit-identical): 0 = planner's choice, 1 = off, 2 = on,
+ * 3 = the default head_dim-40 kernel held to one block per CU (the equal-occupancy reference). */
 void ldm_attention_set_skew(int mode);
 /* Tuning / A-B hook: 1 (default) runs the bf16 backward for head_dim <= 64 on the 32x32x16 MFMA
  * kernels, 0 on the 16x16x16 ones. */
