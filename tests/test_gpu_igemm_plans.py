@@ -252,3 +252,47 @@ def test_splitk_reduction_tiles(B, H, C, Co, ks, plan):
             assert torch.allclose(s, s0, rtol=1e-6, atol=1e-6)
     ref = F.silu(F.conv2d(x, w, b, padding=1) + temb[:, :, None, None]) + resid
     assert rel_err(y0.permute(0, 3, 1, 2), ref) < 2e-2
+
+
+FA_CASES = [
+    # name, B, c0, c1, H, W, Cout, k, stride, up, plan
+    ("3x3", 2, 320, 0, 16, 16, 320, 3, 1, False, (128, 160, 1)),
+    ("3x3_split", 1, 1280, 0, 8, 8, 1280, 3, 1, False, (64, 160, 8)),
+    ("3x3_ring3", 2, 640, 0, 16, 16, 640, 3, 1, False, (128, 160, 4, 3)),
+    ("stride2", 2, 320, 0, 17, 15, 320, 3, 2, False, (64, 160, 2)),
+    ("concat", 2, 640, 320, 16, 16, 320, 3, 1, False, (128, 160, 1)),
+    ("ragged", 1, 64, 0, 20, 20, 200, 3, 1, False, (64, 64, 1)),
+    ("1x1", 3, 640, 0, 10, 10, 960, 1, 1, False, (64, 160, 1)),
+    ("1x1_concat_split", 2, 640, 640, 8, 8, 1280, 1, 1, False, (64, 64, 4)),
+    ("phase_up", 2, 640, 0, 16, 16, 640, 3, 1, True, (0, 0, 1)),
+]
+
+
+@pytest.mark.parametrize("case", FA_CASES, ids=[c[0] for c in FA_CASES])
+def test_fast_addressing_bit_identical(case, plan):
+    """ldm_conv2d_set_fast_addressing: the per-row offsets + wave-uniform K position fetch the same
+    bytes into the same LDS places as the general address walk, so outputs are bit-identical (3x3
+    stride 1 / 2, two-source concat, ragged M / N, 1x1, split K, the 3-stage ring, the phase-form
+    upsample)."""
+    name, B, c0, c1, H, W, Co, k, s, up, pl = case
+    torch.manual_seed(13)
+    x = torch.randn(B, c0 + c1, H, W)
+    w = torch.randn(Co, c0 + c1, k, k) / (k * (c0 + c1) ** 0.5)
+    b = torch.randn(Co)
+    pc = K.PackedConv(w.to(DEV), b.to(DEV), BF, upsample_phases=up)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV, BF)
+    x0 = xn[..., :c0].contiguous()
+    x1 = xn[..., c0:].contiguous() if c1 else None
+    outs = []
+    try:
+        for fa in (False, True):
+            K.set_conv_fast_addressing(fa)
+            if pl[0]:
+                plan(*pl)
+            outs.append(K.conv2d(pc, x0, B, H, W, x1=x1, stride=s, upsample=up, act=K.ACT_SILU))
+    finally:
+        K.set_conv_fast_addressing(True)
+    assert torch.equal(outs[0], outs[1])
+    xr = F.interpolate(x, scale_factor=2.0, mode="nearest") if up else x
+    ref = F.silu(F.conv2d(xr, w, b, stride=s, padding=k // 2))
+    assert rel_err(outs[1].permute(0, 3, 1, 2), ref) < 2e-2

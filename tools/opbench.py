@@ -452,6 +452,8 @@ def main():
                     help="wide-tile persistent 1x1 GEMM modes (ldm_conv2d_set_wide: 0 planner, 1 never, 2 BM 256, 3 BM 128)")
     ap.add_argument("--ring", nargs="*", type=int, default=[0],
                     help="deep-ring 1x1 GEMM modes to compare (ldm_conv2d_set_ring: 0 planner, 1 never, 2 when legal)")
+    ap.add_argument("--fa", nargs="*", type=int, default=[1],
+                    help="tile-kernel fast operand addressing to compare (ldm_conv2d_set_fast_addressing: 0 off, 1 on)")
     ap.add_argument("--skcols", nargs="*", type=int, default=[0],
                     help="split-K reduction tile widths to compare (ldm_conv2d_set_splitk_cols: 0 planner, 64, 128)")
     ap.add_argument("--graph", action="store_true",
@@ -472,12 +474,14 @@ def main():
             continue
         for pl in a.plans:
             for gm in a.groups:
-                for am, sk, wd, rg in [(x, y, z, r) for x in a.ars for y in a.skcols for z in a.wide for r in a.ring]:
+                for am, sk, wd, rg, fa in [(x, y, z, r, f) for x in a.ars for y in a.skcols for z in a.wide for r in a.ring
+                                           for f in a.fa]:
                     run, fl, nb = CASES[n]()
                     f = [0, 0, 1, 0] if pl == "auto" else [int(v) for v in pl.split(",")] + [0]
                     bm, bn, ks, st = f[:4]
 
-                    def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm, am=am, sk=sk, wd=wd, rg=rg):
+                    def run_pl(run=run, bm=bm, bn=bn, ks=ks, st=st, gm=gm, am=am, sk=sk, wd=wd, rg=rg, fa=fa):
+                        K.set_conv_fast_addressing(fa)
                         K.set_conv_splitk_cols(sk)
                         K.force_conv_plan(bm, bn, ks)
                         K.force_conv_stages(st)
@@ -491,7 +495,8 @@ def main():
                     name = name if len(a.ars) == 1 else f"{name}/ars{am}"
                     name = name if len(a.skcols) == 1 else f"{name}/skc{sk}"
                     name = name if len(a.wide) == 1 else f"{name}/w{wd}"
-                    built[name if len(a.ring) == 1 else f"{name}/ring{rg}"] = (run_pl, fl, nb)
+                    name = name if len(a.ring) == 1 else f"{name}/ring{rg}"
+                    built[name if len(a.fa) == 1 else f"{name}/fa{fa}"] = (run_pl, fl, nb)
     for n, (run, _, _) in built.items():
         run()
     torch.cuda.synchronize()

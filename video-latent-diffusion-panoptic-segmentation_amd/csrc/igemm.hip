@@ -34,7 +34,9 @@ int ring_abl();
 
 namespace {
 
-template <typename T, int BM, int BN, bool DMA, int NS = 2>
+// FA: the fast operand addressing of the DMA path (host-side test fast_addressing: tap-major K tiles in
+// one tap and 64-aligned channel block, or a 64-aligned 1x1 conv; no upsampled / dilated gather)
+template <typename T, int BM, int BN, bool DMA, int NS = 2, bool FA = false>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
   constexpr int ES = sizeof(T);
   constexpr int BK = 128 / ES;  // elements per K tile
@@ -215,13 +217,84 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
       }
       advance();
     };
+    // Fast addressing (K tiles that lie in one tap and one channel block of one source — tap-major
+    // K with 64-aligned channels, or a 1x1 conv — and no upsampled / dilated gather): every row's
+    // byte offset without the K position is computed once, the K position is one wave-uniform add
+    // per K tile, and a row's padding taps are a bit mask.  Same bytes to the same LDS places as
+    // issue_dma, with ~30 VALU + ~70 SALU per K tile instead of ~150 + ~240 (runtime mode branches
+    // and a per-row tap walk in a_offset).
+    constexpr bool fast = FA;
+    const int ntaps = p.ksize * p.ksize;
+    int abase0[AI], abase1[AI], bbase[BI];
+    unsigned amask[AI];
+    int f_tap = 0, f_ky = 0, f_kx = 0, f_ch = 0;    // wave-uniform K position of the next tile
+    if constexpr (fast) {
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        unsigned msk = 0;
+        for (int ky = 0; ky < p.ksize; ++ky)
+          for (int kx = 0; kx < p.ksize; ++kx)
+            if (rok[i] && (unsigned)(iy0[i] + ky) < (unsigned)p.h_in && (unsigned)(ix0[i] + kx) < (unsigned)p.w_in)
+              msk |= 1u << (ky * p.ksize + kx);
+        amask[i] = msk;
+        abase0[i] = (pix0[i] * p.c0 + cl * CE) * ES;
+        abase1[i] = (pix0[i] * p.c1 + cl * CE) * ES;
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        const int n = n0 + rr + 32 * i;
+        bbase[i] = n < p.n ? ((wrow0 + n) * p.kpad + cl * CE) * ES : kOOB;
+      }
+      if (p.tap_inner) {
+        const int cb = kt0 / ntaps;
+        f_tap = kt0 - cb * ntaps;
+        f_ch = cb * BK;
+      } else {
+        f_ch = kt0 * BK;
+      }
+      f_ky = f_tap / p.ksize;
+      f_kx = f_tap - f_ky * p.ksize;
+    }
+    auto issue_fast = [&](int buf) {
+#ifdef LDM_ABL_NO_LOADS
+      return;
+#endif
+      const unsigned abase = lds0 + (unsigned)(buf * (BM + BN) * 8 * 16);
+      const unsigned bbl = abase + BM * 8 * 16;
+      const bool kval = f_tap < ntaps && f_ch < p.cin;                 // wave-uniform
+      const bool sel = p.c1 > 0 && f_ch >= p.c0;
+      const int cs = sel ? p.c1 : p.c0;
+      const int ua = ((f_ky * p.w_in + f_kx) * cs + (sel ? f_ch - p.c0 : f_ch)) * ES;
+      const int ub = (f_tap * p.cin + f_ch) * ES;
+      const unsigned tbit = kval ? 1u << f_tap : 0u;
+      const __amdgpu_buffer_rsrc_t ra = sel ? ra1 : ra0;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int off = (amask[i] & tbit) ? (sel ? abase1[i] : abase0[i]) + ua : kOOB;
+        dma16(ra, off, __builtin_amdgcn_readfirstlane(abase + (32 * i + 8 * wv) * 128));
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i)
+        dma16(rw, kval ? bbase[i] + ub : kOOB, __builtin_amdgcn_readfirstlane(bbl + (32 * i + 8 * wv) * 128));
+      if (p.tap_inner) {
+        ++f_tap;
+        if (++f_kx == p.ksize) { f_kx = 0; ++f_ky; }
+        if (f_tap == ntaps) { f_tap = 0; f_ky = 0; f_kx = 0; f_ch += BK; }
+      } else {
+        f_ch += BK;
+      }
+    };
+    auto issue = [&](int kt, int buf) {
+      if constexpr (fast) issue_fast(buf);
+      else issue_dma(kt, buf);
+    };
     if constexpr (NS == 2) {
-      if (kt0 < kt1) issue_dma(kt0, 0);
+      if (kt0 < kt1) issue(kt0, 0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       for (int kt = kt0; kt < kt1; ++kt) {
         const int buf = (kt - kt0) & 1;
-        if (kt + 1 < kt1) issue_dma(kt + 1, buf ^ 1);
+        if (kt + 1 < kt1) issue(kt + 1, buf ^ 1);
         compute(buf);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -234,7 +307,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
       constexpr int PER = AI + BI;
 #pragma unroll
       for (int i = 0; i < NS - 1; ++i)
-        if (kt0 + i < kt1) issue_dma(kt0 + i, i);
+        if (kt0 + i < kt1) issue(kt0 + i, i);
       int st = 0;
       for (int kt = kt0; kt < kt1; ++kt) {
         const int ahead = min(NS - 2, kt1 - 1 - kt);
@@ -243,7 +316,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(const ConvArgs p) {
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         // raw barrier: __syncthreads()' fence would emit vmcnt(0) and drain the tiles in flight
         asm volatile("s_barrier" ::: "memory");
-        if (kt + NS - 1 < kt1) issue_dma(kt + NS - 1, st == 0 ? NS - 1 : st - 1);
+        if (kt + NS - 1 < kt1) issue(kt + NS - 1, st == 0 ? NS - 1 : st - 1);
         compute(st);
         st = st == NS - 1 ? 0 : st + 1;
       }
@@ -1116,6 +1189,17 @@ void launch_splitk_epilogue(const ConvArgs& a, hipStream_t s) {
 
 int g_force_stages = 0;   // tuning hook: 1 register-staged operands, 3 / 4 ring depth, 0 planner
 
+int g_fast_addr = 1;      // A/B hook (ldm_conv2d_set_fast_addressing): 0 keeps the general DMA addressing
+
+// the DMA path's fast operand addressing applies (igemm_kernel's FA)
+bool fast_addressing(const ConvArgs& a, int es) {
+  const int bk = 128 / es;
+  // (>= 8 K tiles: at K = 320 the one-time offset setup is not repaid — to_out 320 at 64x64 22.0 ->
+  // 23.2 us; opbench --fa, profiles/r05y_fast_addressing_ops.txt)
+  return g_fast_addr && !a.upsample && a.ksize <= 5 && a.kpad / bk >= 8 &&
+         (a.tap_inner || (a.ksize == 1 && a.cin % bk == 0 && a.c0 % bk == 0));
+}
+
 template <typename T, int BM, int BN, int NS = 2>
 int launch_bm_bn(ConvArgs a, hipStream_t s) {
   a.tiles_n = (a.n + BN - 1) / BN;
@@ -1123,6 +1207,8 @@ int launch_bm_bn(ConvArgs a, hipStream_t s) {
   a.nblk = tiles_m * a.tiles_n * a.ksplit;
   if (NS == 2 && (a.mixed_src || g_force_stages == 1))
     hipLaunchKernelGGL((igemm_kernel<T, BM, BN, false>), dim3(a.nblk), dim3(256), 0, s, a);
+  else if (fast_addressing(a, sizeof(T)))
+    hipLaunchKernelGGL((igemm_kernel<T, BM, BN, true, NS, true>), dim3(a.nblk), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((igemm_kernel<T, BM, BN, true, NS>), dim3(a.nblk), dim3(256), 0, s, a);
   LDM_CHECK_LAUNCH();
@@ -1459,6 +1545,7 @@ extern "C" void ldm_conv2d_set_halo(int mode) { g_halo_mode = (mode == 1 || mode
 extern "C" void ldm_conv2d_set_halo_split(int ks) { g_halo_split = ks > 0 ? ks : 0; }
 extern "C" void ldm_conv2d_set_halo_rows32(int rows) { g_halo32_rows = (rows == 4 || rows == 8) ? rows : 0; }
 extern "C" void ldm_conv2d_set_ars(int mode) { g_ars_mode = (mode >= 1 && mode <= 3) ? mode : 0; }
+extern "C" void ldm_conv2d_set_fast_addressing(int enabled) { g_fast_addr = enabled ? 1 : 0; }
 extern "C" void ldm_conv2d_set_splitk_cols(int cols) { g_splitk_cols = (cols == 64 || cols == 128) ? cols : 0; }
 extern "C" void ldm_conv2d_set_splitk_rows(int rows) {
   g_splitk_rows = (rows == 16 || rows == 32 || rows == 64) ? rows : 0;

@@ -88,6 +88,7 @@ EXPORTS = {
     "ldm_conv2d_set_ring": (None, [_i]),
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_splitk_rows": (None, [_i]),
+    "ldm_conv2d_set_fast_addressing": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_feedforward": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
     "ldm_transformer_in": (_i, [ctypes.POINTER(GnFold), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
@@ -723,6 +724,11 @@ def set_conv_ring(mode=0):
 def set_conv_splitk_cols(cols=0):
     """Tuning hook: split-K reduction tile width — 0 planner, 64 or 128 forced."""
     load_library().ldm_conv2d_set_splitk_cols(int(cols))
+
+
+def set_conv_fast_addressing(enabled=True):
+    """A/B hook: the tile kernel's fast operand addressing (default on; bit-identical to off)."""
+    load_library().ldm_conv2d_set_fast_addressing(int(bool(enabled)))
 
 
 def set_conv_splitk_rows(rows=0):
