@@ -147,6 +147,9 @@ void ldm_conv2d_set_wide(int mode);
 /* Tuning hook: the deep-ring 1x1 GEMM of the 16x16 / 8x8 levels (csrc/gemm_ring.hip): 0 planner, 1 never,
    2 whenever legal. */
 void ldm_conv2d_set_ring(int mode);
+/* Tuning hook: K splits of the deep-ring kernel's implicit-GEMM 3x3 conv form (and, when > 0, of
+   every ring call): 0 planner (toward one block per CU), > 0 forced (at most 16). */
+void ldm_conv2d_set_ring_split(int ks);
 /* Tuning hook: column width of the split-K reduction kernel's tiles — 0 = planner's choice
  * (64 when 128-wide tiles give fewer than 512 blocks), 64 or 128 forced. */
 /* A/B hook: the tile kernel's fast operand addressing (per-row offsets computed once, the K position

@@ -187,3 +187,61 @@ def test_linear_rows(rows, C, N, act, out_dt, sinusoid):
         if act == K.ACT_SILU:
             ref = F.silu(ref)
     assert rel_err(y, ref) < 2e-2
+
+
+@pytest.mark.parametrize("B,H,c0,c1,N,stride,ks,temb,res", [
+    (8, 8, 1280, 0, 1280, 1, 0, True, False),        # the 8x8 level conv1 (planner: 4 splits)
+    (8, 8, 1280, 0, 1280, 1, 0, False, True),        # conv2 + residual
+    (8, 8, 1280, 1280, 1280, 1, 0, True, False),     # up-block conv1 on the skip concat
+    (8, 16, 1280, 0, 1280, 2, 3, False, False),      # Downsample2D 16 -> 8, 3 splits
+    (3, 8, 640, 0, 320, 1, 7, True, True),           # ragged: 192 rows, 7 splits
+    (2, 8, 640, 0, 640, 1, 1, False, True),          # unsplit ring conv (no time embedding)
+])
+def test_ring_conv3x3(B, H, c0, c1, N, stride, ks, temb, res):
+    """The deep-ring kernel's implicit-GEMM 3x3 form (tap-major 64-deep K steps, per-row tap masks for
+    the zero padding) with K split into fp32 slabs reduced by the split-K kernel (bias, time
+    embedding, residual, GroupNorm partials there).  Its K order differs from the tile kernel's, so
+    it is compared to torch fp32 at the conv tests' 2e-2 and to the tile plan at bf16 rounding; the
+    GroupNorm statistics (fp32 per reduction tile, fp64 across tiles) against the stored output in
+    fp64 at 1e-5."""
+    torch.manual_seed(21)
+    x = torch.randn(B, c0 + c1, H, H)
+    w = torch.randn(N, c0 + c1, 3, 3) / (3 * (c0 + c1) ** 0.5)
+    b = torch.randn(N)
+    ho = H // stride
+    te = torch.randn(B, N) if temb else None
+    r = torch.randn(B, N, ho, ho) if res else None
+    pc = K.PackedConv(w.to(DEV), b.to(DEV), BF)
+    xn = x.permute(0, 2, 3, 1).contiguous().to(DEV, BF)
+    x0 = xn[..., :c0].contiguous()
+    x1 = xn[..., c0:].contiguous() if c1 else None
+    rn = r.permute(0, 2, 3, 1).contiguous().to(DEV, BF) if res else None
+    stats = (ho * ho) % 64 == 0
+
+    def run():
+        return K.conv2d(pc, x0, B, H, H, x1=x1, stride=stride, temb=te.to(DEV) if temb else None,
+                        temb_stride=N, residual=rn, act=K.ACT_SILU if temb else K.ACT_NONE, gn_stats=stats)
+    try:
+        K.set_conv_ring(1)
+        y_tile = run()
+        K.set_conv_ring(2)
+        K.set_conv_ring_split(ks)
+        assert K.describe_plan(B, H, H, c0, N, c1=c1, ksize=3, stride=stride, temb=temb)["kind"] == "ring"
+        y = run()
+    finally:
+        K.set_conv_ring(0)
+        K.set_conv_ring_split(0)
+    ref = F.conv2d(x, w, b, stride=stride, padding=1)
+    if temb:
+        ref = F.silu(ref + te[:, :, None, None])
+    if res:
+        ref = ref + r
+    assert rel_err(y.permute(0, 3, 1, 2), ref) < 2e-2
+    assert rel_err(y, y_tile) < 2e-2
+    if stats:
+        unit = K.gn_unit_for(N)
+        s1 = K.gn_stats_of(y).sum(1)
+        yd = y.double().view(B, ho * ho, N)
+        want = torch.stack([yd.view(B, ho * ho, N // unit, unit).sum((1, 3)),
+                            (yd ** 2).view(B, ho * ho, N // unit, unit).sum((1, 3))], -1)
+        assert torch.allclose(s1, want, rtol=1e-5, atol=1e-5)

@@ -265,6 +265,9 @@ CASES = {
     "conv3_l1_640": lambda: conv_case(8, 32, 32, 640, 640, temb=True, stats=True),
     "conv3_l2_1280": lambda: conv_case(8, 16, 16, 1280, 1280, temb=True, stats=True),
     "conv3_l3_1280": lambda: conv_case(8, 8, 8, 1280, 1280, temb=True, stats=True),
+    "conv3_l3_1280_res": lambda: conv_case(8, 8, 8, 1280, 1280, residual=True, stats=True),
+    "conv3_l3_up_2560": lambda: conv_case(8, 8, 8, 2560, 1280, c1=1280, temb=True, stats=True),
+    "conv3_down_l2": lambda: conv_case(8, 16, 16, 1280, 1280, stride=2, stats=True),
     "conv3_up_l0_960": lambda: conv_case(8, 64, 64, 960, 320, c1=320, residual=True, stats=True),
     "conv3_upsample_640": lambda: conv_case(8, 32, 32, 640, 640, up=True, stats=True),
     "gemm_proj_320": lambda: conv_case(8, 64, 64, 320, 320, k=1, residual=True),
@@ -452,6 +455,7 @@ def main():
                     help="wide-tile persistent 1x1 GEMM modes (ldm_conv2d_set_wide: 0 planner, 1 never, 2 BM 256, 3 BM 128)")
     ap.add_argument("--ring", nargs="*", type=int, default=[0],
                     help="deep-ring 1x1 GEMM modes to compare (ldm_conv2d_set_ring: 0 planner, 1 never, 2 when legal)")
+    ap.add_argument("--rsplit", type=int, default=0, help="ldm_conv2d_set_ring_split for every case")
     ap.add_argument("--fa", nargs="*", type=int, default=[1],
                     help="tile-kernel fast operand addressing to compare (ldm_conv2d_set_fast_addressing: 0 off, 1 on)")
     ap.add_argument("--skcols", nargs="*", type=int, default=[0],
@@ -466,6 +470,7 @@ def main():
     if a.lib:
         K.load_library(os.path.abspath(a.lib))
     K.set_conv_epilogue(a.epi)
+    K.set_conv_ring_split(a.rsplit)
     names = a.only or list(CASES)
     built = {}
     for n in names:

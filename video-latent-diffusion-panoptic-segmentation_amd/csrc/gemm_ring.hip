@@ -81,16 +81,21 @@ __global__ __launch_bounds__(64 * (ring::NL + CWM * CWN), 1) void gemm_ring_kern
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lr = lane & 15, g = lane >> 4;
 
-  // tile: XCD-contiguous ids (blocks b and b + 8 share an XCD), grouped raster over M panels
-  int tm, tn;
+  // tile: XCD-contiguous ids (blocks b and b + 8 share an XCD), grouped raster over M panels; with
+  // split K (ksplit > 1) a tile's splits are adjacent ids and each walks its own range of K steps
+  int tm, tn, split;
   {
     const int nblk = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
-    const int tile = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    int tile = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    split = tile % p.ksplit;
+    tile /= p.ksplit;
     grouped_tile(tile, (p.M + BM - 1) / BM, p.tiles_n, p.group_m, tm, tn);
   }
   const int m0 = tm * BM, n0 = tn * BN;
-  const int nsteps = p.kpad / KS;
+  const int nsteps_all = p.kpad / KS;
+  const int s0 = nsteps_all * split / p.ksplit;
+  const int nsteps = nsteps_all * (split + 1) / p.ksplit - s0;   // this block's K steps
 
   if (tid < FLAG_INTS) flags[tid] = 0;
   __syncthreads();
@@ -120,6 +125,39 @@ __global__ __launch_bounds__(64 * (ring::NL + CWM * CWN), 1) void gemm_ring_kern
     // the swizzle term (4q + (drow >> 1)) & 7 is fixed per wave
     const int drow = lane >> 3;
     const int dchunk = (lane & 7) ^ ((4 * lw + (drow >> 1)) & 7);
+    // this lane's A rows (instruction i: row 8 q + drow, q = lw + NL i < BM / 8): the input pixel of
+    // tap (0, 0) (negative in the padding is fine: only in-image taps are fetched) and a bit per
+    // in-image tap; a 1x1 GEMM has the row itself and one tap
+    const bool conv = p.ksize > 1;
+    int apix[PER];
+    unsigned amsk[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int q = lw + NL * i;
+      const int m = m0 + 8 * q + drow;
+      apix[i] = 0;
+      amsk[i] = 0u;
+      if (8 * q < BM && m < p.M) {
+        if (conv) {
+          const int b = m / p.hw_out, pix = m - b * p.hw_out;
+          const int oy = pix / p.w_out, ox = pix - oy * p.w_out;
+          const int iy0 = oy * p.stride - p.pad, ix0 = ox * p.stride - p.pad;
+          apix[i] = (b * p.h_in + iy0) * p.w_in + ix0;
+          unsigned msk = 0u;
+          for (int ky = 0; ky < p.ksize; ++ky)
+            for (int kx = 0; kx < p.ksize; ++kx)
+              if ((unsigned)(iy0 + ky) < (unsigned)p.h_in && (unsigned)(ix0 + kx) < (unsigned)p.w_in)
+                msk |= 1u << (ky * p.ksize + kx);
+          amsk[i] = msk;
+        } else {
+          apix[i] = m;
+          amsk[i] = 1u;
+        }
+      }
+    }
+    // wave-uniform K position of step s0 + s: K is tap-major and a 64-deep step lies in one tap
+    int ch = (s0 * KS) % p.cin, tap = (s0 * KS) / p.cin;
+    int ky = tap / p.ksize, kx = tap - ky * p.ksize;
     for (int s = 0; s < nsteps + AHEAD; ++s) {
       if (s < nsteps) {
         const int slot = s % NSLOT;
@@ -130,10 +168,13 @@ __global__ __launch_bounds__(64 * (ring::NL + CWM * CWN), 1) void gemm_ring_kern
             __builtin_amdgcn_s_sleep(1);
         }
         const unsigned sbase = lds0 + (unsigned)(slot * SLOT_U4 * 16);
-        const int k0 = s * KS;
-        const int sel = __builtin_amdgcn_readfirstlane((p.c1 > 0 && k0 >= p.c0) ? 1 : 0);   // step-aligned concat
+        const int k0 = (s0 + s) * KS;
+        const int sel = __builtin_amdgcn_readfirstlane((p.c1 > 0 && ch >= p.c0) ? 1 : 0);   // step-aligned concat
         const int cs = sel ? p.c1 : p.c0;
-        const int choff = (sel ? k0 - p.c0 : k0) + dchunk * 8;
+        const int choff = (sel ? ch - p.c0 : ch) + dchunk * 8;
+        const int tapoff = ky * p.w_in + kx;
+        const unsigned tbit = 1u << tap;
+        const __amdgpu_buffer_rsrc_t ra = sel ? ra1 : ra0;
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
           if (p.abl == 2) break;                               // ablation: no operand DMA
@@ -142,10 +183,8 @@ __global__ __launch_bounds__(64 * (ring::NL + CWM * CWN), 1) void gemm_ring_kern
             const unsigned dst = __builtin_amdgcn_readfirstlane(sbase + (unsigned)(q * 1024));
             const int r = 8 * q + drow;
             if (8 * q < BM) {
-              const int m = m0 + r;
-              const int off = m < p.M ? (m * cs + choff) * 2 : kOOB;
-              if (sel) dma16(ra1, off, dst);
-              else dma16(ra0, off, dst);
+              const int off = (amsk[i] & tbit) ? ((apix[i] + tapoff) * cs + choff) * 2 : kOOB;
+              dma16(ra, off, dst);
             } else {
               const int n = n0 + r - BM;
               const int off = n < p.n ? (n * p.kpad + k0 + dchunk * 8) * 2 : kOOB;
@@ -154,6 +193,12 @@ __global__ __launch_bounds__(64 * (ring::NL + CWM * CWN), 1) void gemm_ring_kern
           } else {
             dma16(rw, kOOB, __builtin_amdgcn_readfirstlane(dummy));   // keeps PER instructions per step
           }
+        }
+        ch += KS;
+        if (ch == p.cin) {
+          ch = 0;
+          ++tap;
+          if (++kx == p.ksize) { kx = 0; ++ky; }
         }
       }
       const int t = s - AHEAD;
@@ -223,6 +268,27 @@ __global__ __launch_bounds__(64 * (ring::NL + CWM * CWN), 1) void gemm_ring_kern
     }
   }
   __syncthreads();                                             // ring drained: LDS is the staging area
+
+  if (p.ksplit > 1) {
+    // split K: the raw fp32 tile -> LDS [BM][BN + 4] -> this split's slab as full rows (the
+    // reduction kernel applies bias, time embedding, activation, residual and statistics)
+    constexpr int PITCH = BN + 4;
+    static_assert(BM * PITCH <= MAIN_U4 * 4, "fp32 stage exceeds the ring");
+    float* stage = reinterpret_cast<float*>(smem);
+    if (wave >= NL) {
+      const int cw = wave - NL;
+      const int cwm = cw / CWN, cwn = cw - cwm * CWN;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          *reinterpret_cast<float4*>(stage + (cwm * WM + i * 16 + lr) * PITCH + cwn * WN + j * 16 + 4 * g) =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    }
+    __syncthreads();
+    write_partial_rows<BM, BN, NT>(p, p.partial + (int64_t)split * p.M * p.n, m0, n0, stage, PITCH);
+    return;
+  }
 
   if constexpr (GEGLU) {
     // h * gelu(g) from the accumulators: fragments j (hidden) and j + 1 (gate) hold the two halves of
@@ -316,14 +382,19 @@ namespace ldm_igemm {
 // so every CU owns one tile
 static int g_ring_mode = 0;   // tuning hook (ldm_conv2d_set_ring): 0 planner, 1 never, 2 whenever legal,
                               // 3 / 4: whenever legal in ablation mode 1 (no MFMA) / 2 (no operand DMA)
+static int g_ring_split = 0;  // tuning hook (ldm_conv2d_set_ring_split): 0 planner, > 0 forced K splits
 int ring_abl() { return g_ring_mode >= 3 ? g_ring_mode - 2 : 0; }
 
 bool ring_legal(const ldm_conv_params* q, int es, bool mixed) {
   const auto a16 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; };
-  if (es != 2 || mixed || q->ksize != 1 || q->stride != 1 || q->upsample || q->pad_mode != 0) return false;
-  if (q->c0 % ring::KS || q->c1 % ring::KS || q->kpad % ring::KS || q->kpad != q->c0 + q->c1) return false;
+  // 1x1 GEMMs, and 3x3 convs (stride 1 / 2, zero padding 1) as implicit GEMMs over tap-major K whose
+  // 64-deep steps each lie in one tap of one source
+  if (es != 2 || mixed || q->upsample || q->pad_mode != 0) return false;
+  if (!((q->ksize == 1 && q->stride == 1) || (q->ksize == 3 && (q->stride == 1 || q->stride == 2)))) return false;
+  if (q->c0 % ring::KS || q->c1 % ring::KS || q->kpad % ring::KS) return false;
+  if (q->kpad != q->ksize * q->ksize * (q->c0 + q->c1)) return false;
   if (q->out_layout != LDM_OUT_NHWC && q->out_layout != LDM_OUT_GEGLU) return false;
-  if (q->out_f32 || q->temb) return false;
+  if (q->out_f32) return false;
   if (q->out_layout == LDM_OUT_GEGLU && (q->act != LDM_ACT_NONE || q->residual || q->row_stats || q->gn_partial))
     return false;
   if (!a16(q->out) || !a16(q->bias) || !a16(q->residual) || !a16(q->ln_c1) || (q->n & 7)) return false;
@@ -338,7 +409,26 @@ bool ring_legal(const ldm_conv_params* q, int es, bool mixed) {
 int ring_cfg(const ldm_conv_params* q, int es, bool mixed, int M, bool plan_forced, RingCfg* out) {
   if (g_ring_mode == 1 || plan_forced || !ring_legal(q, es, mixed)) return 0;
   const bool geglu = q->out_layout == LDM_OUT_GEGLU;
-  RingCfg c{0, 0, 0};
+  const int K = q->c0 + q->c1;
+  const int nsteps = q->kpad / ring::KS;
+  if (q->ksize == 3 || g_ring_split > 0) {
+    // 3x3 convs (and forced splits): 128x80 tiles, K split toward one block per CU (>= 16 steps
+    // each); the fp32 slabs go through the split-K reduction kernel, which also applies the time
+    // embedding, residual and GroupNorm partials.  Not planned: at the 8x8 level (B = 8) it ran
+    // 41.9 us against the split 64x160 tiles' 34.2 (3x3 1280, graph-timed; the weight stream of a
+    // 3x3 conv, 29.5 MB read by 4 M tiles, misses L2 where the 1x1 GEMMs' 3.3 MB hits)
+    if (geglu || q->row_stats || q->ln_rows || q->out_layout != LDM_OUT_NHWC || q->n % 80) return 0;
+    const bool want = g_ring_mode >= 2 || g_ring_split > 0;
+    if (!want) return 0;
+    const int tiles = ((M + 127) / 128) * (q->n / 80);
+    int ks = g_ring_split > 0 ? g_ring_split : std::max(1, std::min(16, (256 + tiles / 2) / tiles));
+    ks = std::max(1, std::min(ks, nsteps / 16));
+    if (ks == 1 && q->temb) return 0;                    // (the unsplit ring epilogue has no time embedding)
+    if (out) *out = RingCfg{3, 128, 80, ks};
+    return 3;
+  }
+  if (q->temb) return 0;
+  RingCfg c{0, 0, 0, 1};
   // planner: the B = 8 deep levels (16x16: M = 2048, 8x8: M = 512) and their B = 1..16 neighbours
   // with >= 128 tiles; mode 2 takes any legal M
   const bool any = g_ring_mode >= 2;
@@ -349,9 +439,8 @@ int ring_cfg(const ldm_conv_params* q, int es, bool mixed, int M, bool plan_forc
     // planner range from the graph-timed opbench A/B (profiles/r05d_ring_ops.txt): the ring wins on
     // K <= 2560 at M = 2048 and K <= 1280 at M = 512; the deeper-K ff.net.2 (K = 5120) and the 8x8
     // concat shortcut stay on the split-K tiles, whose partial sums run on more CUs at once
-    const int K = q->c0 + q->c1;
-    if (M >= 1024 && (any || (M <= 2048 && q->n <= 1280 && K <= 2560))) c = {1, 128, 80};
-    else if (M < 1024 && (any || (M >= 256 && q->n <= 1280 && K <= 1280))) c = {2, 32, 80};
+    if (M >= 1024 && (any || (M <= 2048 && q->n <= 1280 && K <= 2560))) c = {1, 128, 80, 1};
+    else if (M < 1024 && (any || (M >= 256 && q->n <= 1280 && K <= 1280))) c = {2, 32, 80, 1};
   }
   if (!c.id) return 0;
   if (!any) {
@@ -365,11 +454,11 @@ int ring_cfg(const ldm_conv_params* q, int es, bool mixed, int M, bool plan_forc
 int launch_ring(ConvArgs a, hipStream_t s, const RingCfg& c) {
   a.tiles_n = a.n / c.bn;
   const int ntiles = ((a.M + c.bm - 1) / c.bm) * a.tiles_n;
-  a.nblk = ntiles;
-  if (c.id == 1)
-    hipLaunchKernelGGL((gemm_ring_kernel<128, 80, 4, 1, 5, 3, false>), dim3(ntiles), dim3(64 * 8), 0, s, a);
+  a.nblk = ntiles * a.ksplit;
+  if (c.id == 1 || c.id == 3)
+    hipLaunchKernelGGL((gemm_ring_kernel<128, 80, 4, 1, 5, 3, false>), dim3(a.nblk), dim3(64 * 8), 0, s, a);
   else if (c.id == 2)
-    hipLaunchKernelGGL((gemm_ring_kernel<32, 80, 2, 1, 8, 5, false>), dim3(ntiles), dim3(64 * 6), 0, s, a);
+    hipLaunchKernelGGL((gemm_ring_kernel<32, 80, 2, 1, 8, 5, false>), dim3(a.nblk), dim3(64 * 6), 0, s, a);
   else
     return LDM_ERR_ARG;
   LDM_CHECK_LAUNCH();
@@ -379,3 +468,4 @@ int launch_ring(ConvArgs a, hipStream_t s, const RingCfg& c) {
 }  // namespace ldm_igemm
 
 extern "C" void ldm_conv2d_set_ring(int mode) { ldm_igemm::g_ring_mode = (mode >= 1 && mode <= 4) ? mode : 0; }
+extern "C" void ldm_conv2d_set_ring_split(int ks) { ldm_igemm::g_ring_split = ks > 0 ? std::min(ks, 16) : 0; }

@@ -1562,9 +1562,10 @@ extern "C" size_t ldm_conv2d_workspace_bytes(const ldm_conv_params* q) {
   const bool mixed = is_mixed(q, es);
   const int hks = halo_plan(q, es, mixed);
   if (hks) return hks > 1 ? (size_t)hks * M * q->n * sizeof(float) : 0;
-  if (ldm_igemm::ring_cfg(q, es, mixed, M, g_force_bm != 0, nullptr) ||
-      ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0) || use_ars(q, es, mixed, M))
-    return 0;
+  ldm_igemm::RingCfg rc{0, 0, 0, 1};
+  if (ldm_igemm::ring_cfg(q, es, mixed, M, g_force_bm != 0, &rc))
+    return rc.ks > 1 ? (size_t)rc.ks * M * q->n * sizeof(float) : 0;
+  if (ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0) || use_ars(q, es, mixed, M)) return 0;
   const Plan pl = make_plan(q, M, es, mixed);
   return pl.ksplit > 1 ? (size_t)pl.ksplit * M * q->n * sizeof(float) : 0;
 }
@@ -1578,9 +1579,9 @@ extern "C" int ldm_conv2d_describe_plan(const ldm_conv_params* q, int* out) {
   const bool mixed = is_mixed(q, es);
   const int hks = halo_plan(q, es, mixed);
   const bool halo = hks > 0;
-  ldm_igemm::RingCfg rc{0, 0, 0};
+  ldm_igemm::RingCfg rc{0, 0, 0, 1};
   if (!halo && ldm_igemm::ring_cfg(q, es, mixed, M, g_force_bm != 0, &rc)) {
-    out[0] = 5; out[1] = rc.bm; out[2] = rc.bn; out[3] = 1; out[4] = 0;
+    out[0] = 5; out[1] = rc.bm; out[2] = rc.bn; out[3] = rc.ks; out[4] = 0;
     return LDM_OK;
   }
   const int wbm = halo ? 0 : ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0);
@@ -1612,11 +1613,13 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   const bool mixed = is_mixed(q, es);
   const int hks = halo_plan(q, es, mixed);
   const bool use_halo = hks > 0;
-  ldm_igemm::RingCfg rc{0, 0, 0};
+  ldm_igemm::RingCfg rc{0, 0, 0, 1};
   const bool ring = !use_halo && ldm_igemm::ring_cfg(q, es, mixed, M, g_force_bm != 0, &rc) != 0;
   const int wbm = (use_halo || ring) ? 0 : ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0);
   const bool ars = !use_halo && !ring && !wbm && use_ars(q, es, mixed, M);
-  const Plan pl = use_halo ? Plan{0, 0, hks} : ((ring || wbm || ars) ? Plan{0, 0, 1} : make_plan(q, M, es, mixed));
+  const Plan pl = use_halo ? Plan{0, 0, hks}
+                           : (ring ? Plan{0, 0, std::max(1, rc.ks)}
+                                   : ((wbm || ars) ? Plan{0, 0, 1} : make_plan(q, M, es, mixed)));
   if (pl.ksplit > 1) {
     const size_t need = (size_t)pl.ksplit * M * q->n * sizeof(float);
     if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;
@@ -1661,7 +1664,9 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   if (use_halo) return launch_halo(a, s);
   if (ring) {
     a.abl = ldm_igemm::ring_abl();
-    return ldm_igemm::launch_ring(a, s, rc);
+    const int st = ldm_igemm::launch_ring(a, s, rc);
+    if (st == LDM_OK && a.ksplit > 1) launch_splitk_epilogue<bf16_t>(a, s);
+    return st;
   }
   if (wbm) return ldm_igemm::launch_wide(a, s, wbm);
   if (ars) return launch_ars(a, s);

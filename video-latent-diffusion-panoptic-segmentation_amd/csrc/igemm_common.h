@@ -41,7 +41,7 @@ struct ConvArgs {
   int abl;            // ablation mode of the deep-ring GEMM (tuning hook; 0 = normal)
 };
 // deep-ring 1x1 GEMM configuration (gemm_ring.hip): id 0 = not the ring kernel
-struct RingCfg { int id, bm, bn; };
+struct RingCfg { int id, bm, bn, ks; };   // ks: K splits (fp32 slabs + the split-K reduction kernel)
 // Storage row of GEMM row m: m itself, or in phase mode (rows ordered (b, phase (dy, dx), y, x) over
 // the h_in x w_in input grid) the output pixel (b, 2y + dy, 2x + dx) of the 2x upsampled image —
 // batch-major either way, so m / hw_out is the batch in both.

@@ -86,6 +86,7 @@ EXPORTS = {
     "ldm_conv2d_set_ars": (None, [_i]),
     "ldm_conv2d_set_wide": (None, [_i]),
     "ldm_conv2d_set_ring": (None, [_i]),
+    "ldm_conv2d_set_ring_split": (None, [_i]),
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_splitk_rows": (None, [_i]),
     "ldm_conv2d_set_fast_addressing": (None, [_i]),
@@ -719,6 +720,11 @@ def set_conv_ring(mode=0):
     """Tuning hook: deep-ring 1x1 GEMM of the 16x16 / 8x8 levels — 0 planner, 1 never, 2 whenever
     legal."""
     load_library().ldm_conv2d_set_ring(int(mode))
+
+
+def set_conv_ring_split(ks=0):
+    """Tuning hook: K splits of the deep-ring kernel (its 3x3 conv form; > 0 forces every ring call)."""
+    load_library().ldm_conv2d_set_ring_split(int(ks))
 
 
 def set_conv_splitk_cols(cols=0):
