@@ -153,9 +153,14 @@ void ldm_conv2d_set_ring_split(int ks);
 /* Tuning hook: column width of the split-K reduction kernel's tiles — 0 = planner's choice
  * (64 when 128-wide tiles give fewer than 512 blocks), 64 or 128 forced. */
 /* A/B hook: the tile kernel's fast operand addressing (per-row offsets computed once, the K position
- * as one wave-uniform add per K tile; tap-major 64-aligned K tiles or 64-aligned 1x1 convs, no
- * upsampled gather): 1 = on (default), 0 = the general per-K-tile address walk.  Bit-identical. */
-void ldm_conv2d_set_fast_addressing(int enabled);
+ * as one wave-uniform add per K tile; tap-major 64-aligned K tiles or 64-aligned 1x1 convs with >= 8
+ * K tiles, no upsampled gather): 4 = planner (default: convs, and 1x1 GEMMs of <= 320 blocks),
+ * 1 = wherever it applies, 2 = convs only, 3 = 1x1 only, 0 = the general per-K-tile address walk.
+ * Bit-identical in every mode. */
+void ldm_conv2d_set_fast_addressing(int mode);
+/* A/B hook: plans of 64-row tiles that give <= 256 blocks (config 2's deep levels) run the 4-stage LDS
+ * ring (three K tiles in flight per block): 1 = on (default), 0 = two stages. */
+void ldm_conv2d_set_fewblock_ring(int enabled);
 void ldm_conv2d_set_splitk_cols(int cols);
 /* Tuning hook: row count of the split-K reduction kernel's tiles — 0 = planner's choice (64, halved
  * down to 16 while the 64-column tiles give fewer than 512 blocks), 16, 32 or 64 forced (16 with

@@ -37,7 +37,7 @@ SKC = [64, 128]     # split-K reduction tile widths (ldm_conv2d_set_splitk_cols;
 
 
 PLANS = [(256, 160, 1, 0), (256, 160, 3, 0), (128, 160, 1, 0), (128, 160, 1, 3), (128, 160, 3, 4), (64, 160, 2, 0),
-         (128, 128, 1, 0), (128, 32, 2, 0), (64, 64, 1, 0), (32, 128, 3, 0)]
+         (128, 128, 1, 0), (128, 32, 2, 0), (64, 64, 1, 0), (32, 128, 3, 0), (64, 160, 3, 4), (64, 64, 2, 4)]
 SHAPES = [
     # name, B, c0, c1, H, W, Cout, k, stride, upsample
     ("l0", 1, 320, 0, 32, 32, 320, 3, 1, False),
@@ -291,7 +291,7 @@ def test_fast_addressing_bit_identical(case, plan):
                 plan(*pl)
             outs.append(K.conv2d(pc, x0, B, H, W, x1=x1, stride=s, upsample=up, act=K.ACT_SILU))
     finally:
-        K.set_conv_fast_addressing(True)
+        K.set_conv_fast_addressing(4)
     assert torch.equal(outs[0], outs[1])
     xr = F.interpolate(x, scale_factor=2.0, mode="nearest") if up else x
     ref = F.silu(F.conv2d(xr, w, b, stride=s, padding=k // 2))

@@ -1189,14 +1189,21 @@ void launch_splitk_epilogue(const ConvArgs& a, hipStream_t s) {
 
 int g_force_stages = 0;   // tuning hook: 1 register-staged operands, 3 / 4 ring depth, 0 planner
 
-int g_fast_addr = 1;      // A/B hook (ldm_conv2d_set_fast_addressing): 0 keeps the general DMA addressing
+int g_fast_addr = 4;      // A/B hook (ldm_conv2d_set_fast_addressing): 0 general DMA addressing, 1 fast,
+                          // 2 fast for convs only, 3 fast for 1x1 only, 4 planner (below)
 
 // the DMA path's fast operand addressing applies (igemm_kernel's FA)
 bool fast_addressing(const ConvArgs& a, int es) {
   const int bk = 128 / es;
   // (>= 8 K tiles: at K = 320 the one-time offset setup is not repaid — to_out 320 at 64x64 22.0 ->
   // 23.2 us; opbench --fa, profiles/r05y_fast_addressing_ops.txt)
-  return g_fast_addr && !a.upsample && a.ksize <= 5 && a.kpad / bk >= 8 &&
+  // mode 4 (default), from same-box A/B of the graph-replayed step (tools/ab_step.py): every conv
+  // (B = 8 neutral), 1x1 GEMMs only with <= 320 blocks — at B = 1 they are latency-bound and gain
+  // (4.29 -> 4.23 ms per step), at B = 8 (512 - 768 blocks) they are throughput-bound and lose
+  // (9.31 -> 9.37 ms)
+  if (g_fast_addr == 4 && a.ksize == 1 && a.nblk > 320) return false;
+  if (!g_fast_addr || (g_fast_addr == 2 && a.ksize == 1) || (g_fast_addr == 3 && a.ksize > 1)) return false;
+  return !a.upsample && a.ksize <= 5 && a.kpad / bk >= 8 &&
          (a.tap_inner || (a.ksize == 1 && a.cin % bk == 0 && a.c0 % bk == 0));
 }
 
@@ -1231,6 +1238,9 @@ int launch_t(const ConvArgs& a, hipStream_t s, int bm, int bn, int stages = 2) {
   if constexpr (sizeof(T) == 2) {
     if (bm == 128 && bn == 160 && !a.mixed_src && stages == 3) return launch_bm_bn<T, 128, 160, 3>(a, s);
     if (bm == 128 && bn == 160 && !a.mixed_src && stages == 4) return launch_bm_bn<T, 128, 160, 4>(a, s);
+    // few-block shapes (config 2's single frame): three K tiles in flight per block
+    if (bm == 64 && bn == 160 && !a.mixed_src && stages == 4) return launch_bm_bn<T, 64, 160, 4>(a, s);
+    if (bm == 64 && bn == 64 && !a.mixed_src && stages == 4) return launch_bm_bn<T, 64, 64, 4>(a, s);
   }
   if (bm == 32) return launch_bm<T, 32>(a, s, bn);
   if (bm == 64) return launch_bm<T, 64>(a, s, bn);
@@ -1261,6 +1271,7 @@ struct Plan {
 
 // Tuning override (ldm_conv2d_force_plan): applied when it is legal for the call.
 int g_force_bm = 0, g_force_bn = 0, g_force_ks = 0;
+int g_fewblock_ring = 1;   // A/B hook (ldm_conv2d_set_fewblock_ring): 0 keeps two stages for <= 256-block 64-row plans
 
 int clamp_ksplit(int ks, int nk) { return std::max(1, std::min(std::min(ks, nk), 16)); }
 
@@ -1305,6 +1316,14 @@ Plan make_plan(const ldm_conv_params* q, int M, int es, bool mixed_src) {
       const int ks = std::max(1, std::min(std::min(16, nk / 4), (512 + t64 / 2) / t64));
       if (t64 * ks >= tiles_now) { pl.bm = 64; pl.bn = 160; pl.ksplit = ks; pl.stages = 2; }
     }
+  }
+  // <= 256 blocks of 64-row tiles (config 2's deep levels: the 8x8 level's 3x3 convs run 128 blocks of
+  // ~11 K tiles, each K tile a dependent HBM round trip with one in flight): a 4-stage LDS ring
+  if (g_fewblock_ring && !g_force_bm && es == 2 && !mixed_src && pl.bm == 64 && (pl.bn == 160 || pl.bn == 64) &&
+      q->out_layout != LDM_OUT_GEGLU) {
+    const int nk = q->kpad / (128 / es);
+    const int blocks = ((M + 63) / 64) * ((q->n + pl.bn - 1) / pl.bn) * pl.ksplit;
+    if (blocks <= 256 && nk / pl.ksplit >= 6) pl.stages = 4;
   }
   if (q->row_stats || q->ln_rows) {
     pl.ksplit = 1;
@@ -1545,7 +1564,8 @@ extern "C" void ldm_conv2d_set_halo(int mode) { g_halo_mode = (mode == 1 || mode
 extern "C" void ldm_conv2d_set_halo_split(int ks) { g_halo_split = ks > 0 ? ks : 0; }
 extern "C" void ldm_conv2d_set_halo_rows32(int rows) { g_halo32_rows = (rows == 4 || rows == 8) ? rows : 0; }
 extern "C" void ldm_conv2d_set_ars(int mode) { g_ars_mode = (mode >= 1 && mode <= 3) ? mode : 0; }
-extern "C" void ldm_conv2d_set_fast_addressing(int enabled) { g_fast_addr = enabled ? 1 : 0; }
+extern "C" void ldm_conv2d_set_fast_addressing(int mode) { g_fast_addr = mode >= 0 && mode <= 4 ? mode : 4; }
+extern "C" void ldm_conv2d_set_fewblock_ring(int enabled) { g_fewblock_ring = enabled ? 1 : 0; }
 extern "C" void ldm_conv2d_set_splitk_cols(int cols) { g_splitk_cols = (cols == 64 || cols == 128) ? cols : 0; }
 extern "C" void ldm_conv2d_set_splitk_rows(int rows) {
   g_splitk_rows = (rows == 16 || rows == 32 || rows == 64) ? rows : 0;

@@ -90,6 +90,7 @@ EXPORTS = {
     "ldm_conv2d_set_splitk_cols": (None, [_i]),
     "ldm_conv2d_set_splitk_rows": (None, [_i]),
     "ldm_conv2d_set_fast_addressing": (None, [_i]),
+    "ldm_conv2d_set_fewblock_ring": (None, [_i]),
     "ldm_conv2d_set_epilogue": (None, [_i]),
     "ldm_feedforward": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
     "ldm_transformer_in": (_i, [ctypes.POINTER(GnFold), ctypes.POINTER(ConvParams), ctypes.POINTER(ConvParams), _vp]),
@@ -732,9 +733,15 @@ def set_conv_splitk_cols(cols=0):
     load_library().ldm_conv2d_set_splitk_cols(int(cols))
 
 
-def set_conv_fast_addressing(enabled=True):
-    """A/B hook: the tile kernel's fast operand addressing (default on; bit-identical to off)."""
-    load_library().ldm_conv2d_set_fast_addressing(int(bool(enabled)))
+def set_conv_fast_addressing(mode=4):
+    """A/B hook: the tile kernel's fast operand addressing — 4 planner (default), 1 / True everywhere it
+    applies, 2 convs only, 3 1x1 only, 0 / False off (bit-identical in every mode)."""
+    load_library().ldm_conv2d_set_fast_addressing(int(mode))
+
+
+def set_conv_fewblock_ring(enabled=True):
+    """A/B hook: 4-stage LDS ring for <= 256-block 64-row tile plans (default on)."""
+    load_library().ldm_conv2d_set_fewblock_ring(int(bool(enabled)))
 
 
 def set_conv_splitk_rows(rows=0):
