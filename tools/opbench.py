@@ -265,6 +265,10 @@ CASES = {
     "conv3_l1_640": lambda: conv_case(8, 32, 32, 640, 640, temb=True, stats=True),
     "conv3_l2_1280": lambda: conv_case(8, 16, 16, 1280, 1280, temb=True, stats=True),
     "conv3_l3_1280": lambda: conv_case(8, 8, 8, 1280, 1280, temb=True, stats=True),
+    "conv_in_16": lambda: conv_case(8, 64, 64, 16, 320, stats=True),
+    "conv_in_16_nostats": lambda: conv_case(8, 64, 64, 16, 320),
+    "conv_in_64_nostats": lambda: conv_case(8, 64, 64, 64, 320),
+    "gemm_320_k64": lambda: conv_case(8, 64, 64, 64, 320, k=1),
     "conv3_l3_1280_res": lambda: conv_case(8, 8, 8, 1280, 1280, residual=True, stats=True),
     "conv3_l3_up_2560": lambda: conv_case(8, 8, 8, 2560, 1280, c1=1280, temb=True, stats=True),
     "conv3_down_l2": lambda: conv_case(8, 16, 16, 1280, 1280, stride=2, stats=True),
