@@ -24,4 +24,4 @@ python3 tools/traffic_table.py --fetch "$OUT/fetch" --write "$OUT/write" --oplog
 python3 tools/step_trace.py "$(ls "$OUT"/stats/*kernel_trace.csv | head -1)" --top 40 > "profiles/${TAG}_step_trace.txt"
 python3 tools/rocprof_summary.py --stats "$OUT/stats" --fetch "$OUT/fetch" --write "$OUT/write" --tag "$TAG" \
   --bench "$OUT/bench_stats.log"
-mkdir -p gpurun_out/profiles && cp profiles/${TAG}_* gpurun_out/profiles/
+mkdir -p gpurun_out/profiles && cp profiles/${TAG}_*.* gpurun_out/profiles/
