@@ -1730,16 +1730,19 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_f8_kernel(const AttnArgs p,
   issue_tile(0, 0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  // full tiles in the loop (no key mask: a runtime `masked` flag had the compiler if-convert the
+  // mask into every tile, 96 VALU per tile and wave), the ragged last tile after it
+  for (int t = 0; t < nfull; ++t) {
     const unsigned scw = scn;
     if (t + 1 < ntiles) {
       scn = scl[(int64_t)(t + 1) * 64];
       issue_tile(t + 1, (t + 1) & 1);
     }
-    compute(t & 1, t * 64, t >= nfull, t == 0, scw);
+    compute(t & 1, t * 64, false, t == 0, scw);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  if (nfull < ntiles) compute(nfull & 1, nfull * 64, true, nfull == 0, scn);
 
   // denominator: O^T row d = 40 = block 1 register 4 of the hh = 0 lane of this column
 #ifdef LDM_F8_DEBUG
