@@ -193,6 +193,17 @@ def gn_case(B, HW, C, stats):
     return run, None, (2 + (0 if stats else 1)) * x.numel() * 2
 
 
+def copy_case(n):
+    """Bandwidth reference: a device copy of n bf16 elements (read + write)."""
+    x = torch.randn(n, device=DEV).to(BF)
+    y = torch.empty_like(x)
+
+    def run():
+        y.copy_(x)
+        return y
+    return run, None, 2 * n * 2
+
+
 def tail_case(B, fused=True, ddim=True):
     """The UNet tail at the 64x64 level: GroupNorm -> SiLU -> conv_out (320 -> 4) (-> DDIM), as one
     ldm_unet_tail launch or the group_norm + conv2d (NCHW) + ddim_step launches it replaces."""
@@ -426,6 +437,7 @@ CASES = {
     "attn_bwd_4096_d40_old": lambda: attn_bwd_case(16, 4096, 320, new=False),
     "attn_bwd_1024_d80": lambda: attn_bwd_case(16, 1024, 640),
     "gn_l0_fused": lambda: gn_case(8, 4096, 320, True),
+    "copy_l0": lambda: copy_case(8 * 4096 * 320),
     "gn_l0_unfused": lambda: gn_case(8, 4096, 320, False),
     "gn_l1_fused": lambda: gn_case(8, 1024, 640, True),
     "gn_l2_fused": lambda: gn_case(8, 256, 1280, True),
