@@ -237,6 +237,17 @@ typedef struct {
 } ldm_attn_params;
 
 int ldm_attention(const ldm_attn_params* p, ldm_stream_t stream);
+/* As ldm_attention, with a caller workspace that lets the bf16 head_dim-40 path split the keys
+ * when the (batch, heads, n_q) grid alone would leave the GPU under-occupied (a single frame of the
+ * 64x64 level: 128 eight-wave query blocks): each split writes a normalised fp32 partial and its
+ * log-sum-exp to the workspace and a merge kernel combines them (same math, different fp32
+ * summation order).  ldm_attention_workspace_bytes returns 0 when no split applies; then the call
+ * is exactly ldm_attention and the workspace may be NULL. */
+size_t ldm_attention_workspace_bytes(const ldm_attn_params* p);
+int ldm_attention_ws(const ldm_attn_params* p, void* workspace, int64_t workspace_bytes, ldm_stream_t stream);
+/* Tuning / A-B hook for the split: -1 planner (default), 0 or 1 off, k >= 2 forced (at most 8 and
+ * n_kv / 128 splits). */
+void ldm_attention_set_kvsplit(int splits);
 /* BASELINE config 5 ("fp8 MFMA attention", pose-conditioned video LDM at T=16): as ldm_attention
  * (bf16 inputs and output).
  *   head_dim 40 (16-byte row strides): BOTH products on the block-scaled

@@ -5,6 +5,8 @@ otherwise plain torch fp32 on the CPU (floating-point kernels).
 Tolerances (stated per test): fp32 path 1e-4 relative to the tensor scale (exact fp32 MFMA,
 only summation order differs); bf16 path 2e-2 (8-bit mantissa storage, fp32 accumulate).
 """
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -329,11 +331,13 @@ def test_attention_d40_qs2_close_to_default(B, N):
                      for b in range(B)]).permute(0, 2, 1, 3).reshape(B, N, C)
     outs = []
     try:
+        K.set_attention_kvsplit(0)          # mode 0 = the unsplit default kernel
         for mode in (0, 1, 2):
             K.set_attention_qs2(mode)
             outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, 40, N, N, 3 * C, 3 * C, 3 * C).float())
     finally:
         K.set_attention_qs2(0)
+        K.set_attention_kvsplit(-1)
     for o in outs:
         assert ((o - ref).norm() / ref.norm()).item() < 1e-2
     assert (outs[0] - outs[1]).abs().max().item() < 0.05
@@ -366,6 +370,54 @@ def test_attention_skew_bit_identical(B, N, hd):
     x = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
     ref = (torch.softmax(x[0] @ x[1].transpose(-1, -2) * hd ** -0.5, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B, N, C)
     assert ((outs[1][0].float() - ref).norm() / ref.norm()).item() < 1e-2
+
+
+@pytest.mark.parametrize("B,N,splits", [(1, 4096, -1), (1, 4096 + 37, -1), (1, 64 * 5 + 3, 3), (1, 300, 2),
+                                         (2, 1024, 8), (1, 4096, 3), (1, 256 + 1, 2)])
+def test_attention_kvsplit(B, N, splits):
+    """ldm_attention_ws: head_dim 40 with the keys split over blocks (fp32 partials + log-sum-exp,
+    merged by attn_kv_combine) against torch fp32 and against the unsplit kernel; a large logit sits
+    in the last key tile so the merge's rescale is exercised."""
+    torch.manual_seed(12)
+    hd, H = 40, 8
+    C = H * hd
+    q, k, v = torch.randn(B, N, C), torch.randn(B, N, C), torch.randn(B, N, C)
+    k[0, N - 2] = q[0, 5] * 4.0
+    qkv = torch.cat([q, k, v], -1).to(DEV).to(torch.bfloat16)
+    try:
+        K.set_attention_kvsplit(0)
+        o0 = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C, 3 * C)
+        K.set_attention_kvsplit(splits)
+        p = K.AttnParams(0, 0, 0, 0, 3 * C, 3 * C, 3 * C, C, B, H, hd, N, N, hd ** -0.5, K.dtype_code(torch.bfloat16))
+        p.q = p.k = p.v = p.o = 1 << 20              # any 16-byte-aligned address: sizing only
+        assert K.load_library().ldm_attention_workspace_bytes(ctypes.byref(p)) > 0
+        o1 = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C, 3 * C)
+    finally:
+        K.set_attention_kvsplit(-1)
+    x = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(x[0] @ x[1].transpose(-1, -2) * hd ** -0.5, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B, N, C)
+    assert rel_err(o1, ref) < 1e-2
+    assert rel_err(o1, o0.float()) < 1e-2
+    # P is rounded to bf16 against a different running max per split, so not bit-identical to the
+    # one-pass kernel: the same bound as the qs2 form, and no worse against fp32 than the one pass
+    assert (o1.float() - o0.float()).abs().max().item() < 0.05
+    assert rel_err(o1, ref) <= 1.2 * rel_err(o0, ref) + 1e-4
+
+
+def test_attention_kvsplit_planner():
+    """The planner splits only the under-occupied single-frame head_dim-40 case."""
+    lib = K.load_library()
+
+    def ws(B, N, hd=40, H=8):
+        p = K.AttnParams(1 << 20, 1 << 20, 1 << 20, 1 << 20, 3 * H * hd, 3 * H * hd, 3 * H * hd, H * hd, B, H, hd, N, N,
+                         hd ** -0.5, K.dtype_code(torch.bfloat16))
+        return int(lib.ldm_attention_workspace_bytes(ctypes.byref(p)))
+
+    assert ws(1, 4096) > 0
+    assert ws(8, 4096) == 0            # 1024 query blocks already
+    assert ws(1, 4096, hd=80, H=8) == 0
+    assert ws(1, 77) == 0              # a single key tile
+    assert ws(4, 197) == 0             # 32 query blocks but only 4 key tiles
 
 
 def test_attention_softmax_spike():

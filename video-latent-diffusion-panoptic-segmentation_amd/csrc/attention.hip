@@ -25,6 +25,10 @@ struct AttnArgs {
   int heads, d, nq, nkv;
   float scale_log2;
   float* lse;         // optional [batch][heads][nq]: log2-domain log-sum-exp (training forward)
+  int kvsplit;        // > 1: attn_d40_kernel<..., KVS> splits the keys; partials in opart / lsepart
+  int batch;
+  float* opart;       // [kvsplit][batch][heads][nq][d] normalised fp32 partial outputs
+  float* lsepart;     // [kvsplit][batch][heads][nq] their log2-domain log-sum-exp
 };
 
 __device__ const uint4 kZeros16 = {0u, 0u, 0u, 0u};
@@ -689,7 +693,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 // and their order are unchanged (bit-identical); V of tile t - 1 stays readable, so three K/V buffers.
 // (__launch_bounds__' second argument is waves per SIMD: OCC blocks of NW waves need OCC * NW / 4; the
 // default form meets it at 127 VGPRs unasked, the SKEW form is held to it)
-template <int NW, int OCC, int KT = 64, int D = 40, int QS = 1, bool SKEW = false>
+// KVS: split-KV (config 2's single frame: 256 four-wave blocks left one wave per SIMD): block id =
+// (query block, split); the split walks key tiles [t0, t1) and writes its normalised fp32 output and
+// log-sum-exp, which attn_kv_combine merges
+template <int NW, int OCC, int KT = 64, int D = 40, int QS = 1, bool SKEW = false, bool KVS = false>
 __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p) {
   typedef bf16_t T;
   typedef __attribute__((ext_vector_type(16))) float f32x16_t;
@@ -706,17 +713,25 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r32 = lane & 31, hh = lane >> 5, i16 = lane & 15;
-  int qb, h, b;
+  int qb, h, b, split = 0;
   {
     const int nqb = (p.nq + 32 * QS * NW - 1) / (32 * QS * NW);
     const int bid = blockIdx.x, nblk = gridDim.x;
     const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
-    const int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    if constexpr (KVS) {
+      split = t % p.kvsplit;
+      t /= p.kvsplit;
+    }
     qb = t % nqb;
     const int hb = t / nqb;
     h = hb % p.heads;
     b = hb / p.heads;
   }
+  static_assert(!(SKEW && KVS), "split-KV has one phase");
+  const int ntiles_all = (p.nkv + KT - 1) / KT;
+  const int t0 = KVS ? ntiles_all * split / p.kvsplit : 0;               // this block's key tiles
+  const int t1 = KVS ? ntiles_all * (split + 1) / p.kvsplit : ntiles_all;
   // a wave owns QS subtiles of 32 queries: qbase + 32 s + r32
   const int qbase = qb * (32 * QS * NW) + wave * (32 * QS);
   const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
@@ -758,9 +773,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
     const int row = L / RCH, c = L - row * RCH;
     const bool dat = i < RCH * (KT / 64) && c < CPR && c * EPC < p.d;
     const bool one = c == ONES_CHUNK;
-    kq[s2] = dat ? reinterpret_cast<const char*>(kp + (int64_t)(KT + row) * p.ks + c * EPC)
+    kq[s2] = dat ? reinterpret_cast<const char*>(kp + (int64_t)((t0 + 1) * KT + row) * p.ks + c * EPC)
                  : reinterpret_cast<const char*>(one ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
-    vq[s2] = dat ? reinterpret_cast<const char*>(vp + (int64_t)(KT + row) * p.vs + c * EPC)
+    vq[s2] = dat ? reinterpret_cast<const char*>(vp + (int64_t)((t0 + 1) * KT + row) * p.vs + c * EPC)
                  : reinterpret_cast<const char*>(one ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
     kstep[s2] = dat ? (int64_t)KT * p.ks * ES : 0;
     vstep[s2] = dat ? (int64_t)KT * p.vs * ES : 0;
@@ -925,21 +940,21 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
     smpv(sacc, buf, half, first && half == 0);
   };
 
-  const int ntiles = (p.nkv + KT - 1) / KT;
-  const int nfull = p.nkv / KT;
+  const int ntiles = t1;                                   // (tiles t0 .. t1 - 1 are this block's)
+  const int nfull = min(p.nkv / KT, t1);
   auto bufi = [](int t) { return NB == 3 ? t % 3 : t & 1; };
   auto issue_next = [&](int t) {   // tile t + 1 while tile t is multiplied
     if (t + 1 < nfull) issue_full(bufi(t + 1));
     else if (t + 1 < ntiles) issue_tile((t + 1) * KT, bufi(t + 1));
   };
-  issue_tile(0, 0);
+  issue_tile(t0 * KT, bufi(t0));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if constexpr (!SKEW) {
-    for (int t = 0; t < nfull; ++t) {
+    for (int t = t0; t < nfull; ++t) {
       issue_next(t);
 #pragma unroll
-      for (int hf = 0; hf < KT / 64; ++hf) compute(bufi(t), t * KT, false, t == 0, hf);
+      for (int hf = 0; hf < KT / 64; ++hf) compute(bufi(t), t * KT, false, t == t0, hf);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
@@ -974,9 +989,10 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
       }
     }
   }
-  if (nfull < ntiles) {
-    for (int hf = 0; hf < KT / 64 && nfull * KT + 64 * hf < p.nkv; ++hf)
-      compute(bufi(nfull), nfull * KT, true, nfull == 0, hf);
+  if (max(nfull, t0) < ntiles) {
+    const int tr = max(nfull, t0);                           // the ragged last tile
+    for (int hf = 0; hf < KT / 64 && tr * KT + 64 * hf < p.nkv; ++hf)
+      compute(bufi(tr), tr * KT, true, tr == t0, hf);
   }
 
   // denominator: O^T row d = D = block D / 32, register 4 ((D % 32) / 8) of the hh = 0 lane of this
@@ -987,7 +1003,21 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
     const float lt = __shfl(oacc[s][D / 32][4 * ((D % 32) / 8)], r32, 64);
     const float inv = 1.0f / lt;
     const int qi = qbase + 32 * s + r32;
-    if (qi < p.nq) {
+    if (KVS && qi < p.nq) {
+      // this split's normalised output and log-sum-exp (fp32) for attn_kv_combine
+      const int64_t row = ((int64_t)split * p.batch + b) * p.heads * p.nq + (int64_t)h * p.nq + qi;
+      if (hh == 0) p.lsepart[row] = mq[s] + __log2f(lt);
+      float* orow = p.opart + row * D;
+#pragma unroll
+      for (int db = 0; db < ND32; ++db)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int d = 32 * db + 8 * g4 + 4 * hh;
+          if (32 * db + 8 * g4 >= D) break;
+          *reinterpret_cast<float4*>(orow + d) = make_float4(oacc[s][db][4 * g4] * inv, oacc[s][db][4 * g4 + 1] * inv,
+                                                             oacc[s][db][4 * g4 + 2] * inv, oacc[s][db][4 * g4 + 3] * inv);
+        }
+    } else if (qi < p.nq) {
       if (p.lse && hh == 0) p.lse[((int64_t)b * p.heads + h) * p.nq + qi] = mq[s] + __log2f(lt);
       T* orow = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * p.d + (int64_t)qi * p.os;
 #pragma unroll
@@ -1318,6 +1348,67 @@ int launch32_dp_mc(const AttnArgs& a, int batch, hipStream_t s) {
   }
   if (a.d == DP - 8) return launch32_cfg<DP, QS1, true, F8, MC>(a, batch, s);
   return launch32_cfg<DP, QS0, false, F8, MC>(a, batch, s);
+}
+
+// split-KV merge: one thread per (row = (b, h, q), 4 head-dim columns); the splits' fp32 partials
+// are weighted by 2^(lse_s - max lse) (log2 domain, like the kernels' lse) and summed in split order
+template <int D>
+__global__ __launch_bounds__(256) void attn_kv_combine(const AttnArgs p) {
+  constexpr int NC = D / 4;
+  const int64_t rows = (int64_t)p.batch * p.heads * p.nq;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= rows * NC) return;
+  const int64_t row = gid / NC;
+  const int c4 = (int)(gid - row * NC);
+  float m = -INFINITY;
+  for (int sp = 0; sp < p.kvsplit; ++sp) m = fmaxf(m, p.lsepart[sp * rows + row]);
+  float den = 0.f;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int sp = 0; sp < p.kvsplit; ++sp) {
+    const float w = exp2f(p.lsepart[sp * rows + row] - m);
+    const float4 o = *reinterpret_cast<const float4*>(p.opart + (sp * rows + row) * D + 4 * c4);
+    den += w;
+    acc.x += w * o.x; acc.y += w * o.y; acc.z += w * o.z; acc.w += w * o.w;
+  }
+  const float inv = 1.0f / den;
+  const int qi = (int)(row % p.nq);
+  const int64_t bh = row / p.nq;
+  const int h = (int)(bh % p.heads), b = (int)(bh / p.heads);
+  if (p.lse && c4 == 0) p.lse[row] = m + __log2f(den);
+  bf16_t* orow = reinterpret_cast<bf16_t*>(p.o) + ((int64_t)b * p.nq + qi) * p.os + (int64_t)h * p.d + 4 * c4;
+  *reinterpret_cast<uint2*>(orow) = make_uint2(pack_bf16x2(acc.x * inv, acc.y * inv), pack_bf16x2(acc.z * inv, acc.w * inv));
+}
+
+int g_attn_kvsplit = -1;   // tuning / A-B hook (ldm_attention_set_kvsplit): -1 planner, 0 off, k >= 2 forced
+
+// split count for head_dim 40 bf16: enough (query block, split) 8-wave blocks for two per CU; 1 = no split
+int kv_splits(const AttnArgs& a, int batch) {
+  if (a.d != 40 || g_attn_kvsplit == 0) return 1;
+  const int nblk = (a.nq + 255) / 256 * a.heads * batch;
+  const int ntiles = (a.nkv + 63) / 64;
+  int sp = g_attn_kvsplit > 0 ? g_attn_kvsplit : (nblk >= 512 ? 1 : (512 + nblk - 1) / nblk);
+  // the planner keeps >= 4 key tiles per split (a short sequence is launch-bound: the merge
+  // kernel would cost more than the occupancy buys); forced splits go down to 2 tiles
+  sp = min(sp, min(8, ntiles / (g_attn_kvsplit > 0 ? 2 : 4)));
+  return sp >= 2 ? sp : 1;
+}
+
+size_t kv_workspace(const AttnArgs& a, int batch) {
+  const int sp = kv_splits(a, batch);
+  if (sp < 2) return 0;
+  const size_t rows = (size_t)batch * a.heads * a.nq;
+  return (size_t)sp * rows * (40 * 4 + 4) + 256;
+}
+
+// split-KV launch: the partials kernel then the merge; a (with kvsplit, opart, lsepart) set by the caller
+int launch_kv_split(const AttnArgs& a, int batch, hipStream_t s) {
+  const int nblk = (a.nq + 255) / 256 * a.heads * batch * a.kvsplit;
+  hipLaunchKernelGGL((attn_d40_kernel<8, 2, 64, 40, 1, false, true>), dim3(nblk), dim3(512), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  const int64_t n = (int64_t)batch * a.heads * a.nq * 10;
+  hipLaunchKernelGGL((attn_kv_combine<40>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  LDM_CHECK_LAUNCH();
+  return LDM_OK;
 }
 
 int g_attn_d80 = 1;      // tuning / A-B hook: 0 routes head_dim 80 to the 16x16x32 kernel
@@ -2534,6 +2625,8 @@ AttnArgs attn_args(const ldm_attn_params* q) {
   a.heads = q->heads; a.d = q->head_dim; a.nq = q->n_q; a.nkv = q->n_kv;
   a.scale_log2 = q->scale * 1.4426950408889634f;
   a.lse = nullptr;
+  a.kvsplit = 1; a.batch = q->batch;
+  a.opart = nullptr; a.lsepart = nullptr;
   return a;
 }
 }  // namespace
@@ -2553,6 +2646,31 @@ bool fp8_scaled_ok(const ldm_attn_params* q) {
          q->o_stride % 4 == 0;
 }
 }  // namespace
+
+extern "C" size_t ldm_attention_workspace_bytes(const ldm_attn_params* q) {
+  if (attn_validate(q) != LDM_OK || q->dtype != LDM_BF16 || g_attn_legacy || g_attn_d40 == 0 || g_attn_waves || g_attn_qs2 || q->q_stride % 8 ||
+      q->o_stride % 4)
+    return 0;
+  return kv_workspace(attn_args(q), q->batch);
+}
+
+extern "C" int ldm_attention_ws(const ldm_attn_params* q, void* workspace, int64_t workspace_bytes,
+                                ldm_stream_t stream) {
+  const int st = attn_validate(q);
+  if (st != LDM_OK) return st;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const size_t need = ldm_attention_workspace_bytes(q);
+  if (need == 0) return ldm_attention(q, stream);
+  if (!workspace || workspace_bytes < (int64_t)need || !aligned16(workspace)) return LDM_ERR_ARG;
+  AttnArgs a = attn_args(q);
+  a.kvsplit = kv_splits(a, q->batch);
+  const size_t rows = (size_t)q->batch * q->heads * q->n_q;
+  a.opart = static_cast<float*>(workspace);
+  a.lsepart = a.opart + (size_t)a.kvsplit * rows * 40;
+  return launch_kv_split(a, q->batch, s);
+}
+
+extern "C" void ldm_attention_set_kvsplit(int splits) { g_attn_kvsplit = splits < 0 ? -1 : (splits == 1 ? 0 : splits); }
 
 extern "C" size_t ldm_attention_fp8_workspace_bytes(const ldm_attn_params* q) {
   if (attn_validate(q) != LDM_OK || q->dtype != LDM_BF16 || !fp8_scaled_ok(q)) return 0;

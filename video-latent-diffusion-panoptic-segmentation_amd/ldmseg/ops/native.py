@@ -97,6 +97,9 @@ EXPORTS = {
     "ldm_transformer_in_set_mode": (None, [_i]),
     "ldm_attention": (_i, [ctypes.POINTER(AttnParams), _vp]),
     "ldm_attention_fp8": (_i, [ctypes.POINTER(AttnParams), _vp, _i64, _vp]),
+    "ldm_attention_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
+    "ldm_attention_ws": (_i, [ctypes.POINTER(AttnParams), _vp, _i64, _vp]),
+    "ldm_attention_set_kvsplit": (None, [_i]),
     "ldm_attention_fp8_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_set_fp8_scaled": (None, [_i]),
     "ldm_attention_set_maxcol": (None, [_i]),
@@ -674,6 +677,12 @@ def set_attention_skew(mode=0):
     load_library().ldm_attention_set_skew(int(mode))
 
 
+def set_attention_kvsplit(splits=-1):
+    """Tuning / A-B hook for head_dim 40 bf16 split-KV (ldm_attention_ws): -1 planner, 0 / 1 off,
+    k >= 2 forced."""
+    load_library().ldm_attention_set_kvsplit(int(splits))
+
+
 def force_attention_legacy(legacy=True):
     """Tuning hook: route bf16 attention through the 16x16x16-MFMA kernel (A/B only)."""
     load_library().ldm_attention_force_legacy(int(bool(legacy)))
@@ -947,7 +956,12 @@ def attention(q, k, v, batch, heads, head_dim, n_q, n_kv, q_stride, k_stride, v_
         ws = torch.empty(wsb, dtype=torch.uint8, device=q.device) if wsb else None
         _check(lib.ldm_attention_fp8(ctypes.byref(p), _ptr(ws), wsb, _stream(q)), "ldm_attention_fp8")
     else:
-        _check(lib.ldm_attention(ctypes.byref(p), _stream(q)), "ldm_attention")
+        wsb = int(lib.ldm_attention_workspace_bytes(ctypes.byref(p)))
+        if wsb:
+            ws = torch.empty(wsb, dtype=torch.uint8, device=q.device)
+            _check(lib.ldm_attention_ws(ctypes.byref(p), _ptr(ws), wsb, _stream(q)), "ldm_attention_ws")
+        else:
+            _check(lib.ldm_attention(ctypes.byref(p), _stream(q)), "ldm_attention")
     _prof_stop(ev, "attention", 4.0 * batch * heads * n_q * n_kv * head_dim,
                (2 * batch * n_q * C + 2 * batch * n_kv * C) * q.element_size(), f"N={n_q} L={n_kv} d={head_dim}")
     return out
