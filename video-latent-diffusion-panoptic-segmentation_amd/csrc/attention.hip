@@ -941,7 +941,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   };
 
   const int ntiles = t1;                                   // (tiles t0 .. t1 - 1 are this block's)
-  const int nfull = min(p.nkv / KT, t1);
+  const int nfull = KVS ? min(p.nkv / KT, t1) : p.nkv / KT;
   auto bufi = [](int t) { return NB == 3 ? t % 3 : t & 1; };
   auto issue_next = [&](int t) {   // tile t + 1 while tile t is multiplied
     if (t + 1 < nfull) issue_full(bufi(t + 1));
@@ -989,8 +989,8 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
       }
     }
   }
-  if (max(nfull, t0) < ntiles) {
-    const int tr = max(nfull, t0);                           // the ragged last tile
+  const int tr = KVS ? max(nfull, t0) : nfull;             // the ragged last tile
+  if (tr < ntiles) {
     for (int hf = 0; hf < KT / 64 && tr * KT + 64 * hf < p.nkv; ++hf)
       compute(bufi(tr), tr * KT, true, tr == t0, hf);
   }
