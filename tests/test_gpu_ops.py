@@ -374,12 +374,13 @@ def test_attention_skew_bit_identical(B, N, hd):
 
 @pytest.mark.parametrize("B,N,splits", [(1, 4096, -1), (1, 4096 + 37, -1), (1, 64 * 5 + 3, 3), (1, 300, 2),
                                          (2, 1024, 8), (1, 4096, 3), (1, 256 + 1, 2)])
-def test_attention_kvsplit(B, N, splits):
+@pytest.mark.parametrize("hd", [40, 80])
+def test_attention_kvsplit(B, N, splits, hd):
     """ldm_attention_ws: head_dim 40 with the keys split over blocks (fp32 partials + log-sum-exp,
     merged by attn_kv_combine) against torch fp32 and against the unsplit kernel; a large logit sits
     in the last key tile so the merge's rescale is exercised."""
     torch.manual_seed(12)
-    hd, H = 40, 8
+    H = 8
     C = H * hd
     q, k, v = torch.randn(B, N, C), torch.randn(B, N, C), torch.randn(B, N, C)
     k[0, N - 2] = q[0, 5] * 4.0
@@ -415,7 +416,9 @@ def test_attention_kvsplit_planner():
 
     assert ws(1, 4096) > 0
     assert ws(8, 4096) == 0            # 1024 query blocks already
-    assert ws(1, 4096, hd=80, H=8) == 0
+    assert ws(1, 1024, hd=80) > 0      # 32 eight-wave blocks at the 32x32 level
+    assert ws(8, 1024, hd=80) == 0     # 256 already
+    assert ws(1, 256, hd=160) == 0
     assert ws(1, 77) == 0              # a single key tile
     assert ws(4, 197) == 0             # 32 query blocks but only 4 key tiles
 

@@ -1379,17 +1379,21 @@ __global__ __launch_bounds__(256) void attn_kv_combine(const AttnArgs p) {
   *reinterpret_cast<uint2*>(orow) = make_uint2(pack_bf16x2(acc.x * inv, acc.y * inv), pack_bf16x2(acc.z * inv, acc.w * inv));
 }
 
+int g_attn_d80 = 1;      // tuning / A-B hook: 0 routes head_dim 80 to the 16x16x32 kernel
 int g_attn_kvsplit = -1;   // tuning / A-B hook (ldm_attention_set_kvsplit): -1 planner, 0 off, k >= 2 forced
 
-// split count for head_dim 40 bf16: enough (query block, split) 8-wave blocks for two per CU; 1 = no split
+// split count: head_dim 40 — enough (query block, split) 8-wave blocks for two per CU, >= 4 key
+// tiles per split; head_dim 80 (one 8-wave block per CU) — 256 blocks, >= 2 key tiles per split;
+// 1 = no split
 int kv_splits(const AttnArgs& a, int batch) {
-  if (a.d != 40 || g_attn_kvsplit == 0) return 1;
+  if (g_attn_kvsplit == 0 || !(a.d == 40 || (a.d == 80 && g_attn_d80))) return 1;
   const int nblk = (a.nq + 255) / 256 * a.heads * batch;
+  const int target = a.d == 40 ? 512 : 256;
   const int ntiles = (a.nkv + 63) / 64;
-  int sp = g_attn_kvsplit > 0 ? g_attn_kvsplit : (nblk >= 512 ? 1 : (512 + nblk - 1) / nblk);
-  // the planner keeps >= 4 key tiles per split (a short sequence is launch-bound: the merge
-  // kernel would cost more than the occupancy buys); forced splits go down to 2 tiles
-  sp = min(sp, min(8, ntiles / (g_attn_kvsplit > 0 ? 2 : 4)));
+  int sp = g_attn_kvsplit > 0 ? g_attn_kvsplit : (nblk >= target ? 1 : (target + nblk - 1) / nblk);
+  // the planner keeps >= 4 key tiles per split at d = 40 (a short sequence is launch-bound: the
+  // merge kernel would cost more than the occupancy buys); forced splits go down to 2 tiles
+  sp = min(sp, min(8, ntiles / (g_attn_kvsplit > 0 || a.d == 80 ? 2 : 4)));
   return sp >= 2 ? sp : 1;
 }
 
@@ -1397,21 +1401,26 @@ size_t kv_workspace(const AttnArgs& a, int batch) {
   const int sp = kv_splits(a, batch);
   if (sp < 2) return 0;
   const size_t rows = (size_t)batch * a.heads * a.nq;
-  return (size_t)sp * rows * (40 * 4 + 4) + 256;
+  return (size_t)sp * rows * (a.d * 4 + 4) + 256;
 }
 
 // split-KV launch: the partials kernel then the merge; a (with kvsplit, opart, lsepart) set by the caller
 int launch_kv_split(const AttnArgs& a, int batch, hipStream_t s) {
   const int nblk = (a.nq + 255) / 256 * a.heads * batch * a.kvsplit;
-  hipLaunchKernelGGL((attn_d40_kernel<8, 2, 64, 40, 1, false, true>), dim3(nblk), dim3(512), 0, s, a);
-  LDM_CHECK_LAUNCH();
-  const int64_t n = (int64_t)batch * a.heads * a.nq * 10;
-  hipLaunchKernelGGL((attn_kv_combine<40>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  const int64_t n = (int64_t)batch * a.heads * a.nq * (a.d / 4);
+  if (a.d == 40) {
+    hipLaunchKernelGGL((attn_d40_kernel<8, 2, 64, 40, 1, false, true>), dim3(nblk), dim3(512), 0, s, a);
+    LDM_CHECK_LAUNCH();
+    hipLaunchKernelGGL((attn_kv_combine<40>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80, 1, false, true>), dim3(nblk), dim3(512), 0, s, a);
+    LDM_CHECK_LAUNCH();
+    hipLaunchKernelGGL((attn_kv_combine<80>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  }
   LDM_CHECK_LAUNCH();
   return LDM_OK;
 }
 
-int g_attn_d80 = 1;      // tuning / A-B hook: 0 routes head_dim 80 to the 16x16x32 kernel
 int g_attn_skew = 0;     // tuning / A-B hook (ldm_attention_set_skew): 0 planner, 1 off, 2 on
 int g_attn_qs2 = 0;      // tuning / A-B hook: head_dim 40 as 64 queries per wave: 1 two subtiles in step,
                          // 2 the pipelined form (attn_d40p_kernel)
@@ -2648,7 +2657,8 @@ bool fp8_scaled_ok(const ldm_attn_params* q) {
 }  // namespace
 
 extern "C" size_t ldm_attention_workspace_bytes(const ldm_attn_params* q) {
-  if (attn_validate(q) != LDM_OK || q->dtype != LDM_BF16 || g_attn_legacy || g_attn_d40 == 0 || g_attn_waves || g_attn_qs2 || q->q_stride % 8 ||
+  if (attn_validate(q) != LDM_OK || q->dtype != LDM_BF16 || g_attn_legacy || (q->head_dim == 40 && g_attn_d40 == 0) || g_attn_waves || g_attn_qs2 ||
+      q->q_stride % 8 ||
       q->o_stride % 4)
     return 0;
   return kv_workspace(attn_args(q), q->batch);
@@ -2666,7 +2676,7 @@ extern "C" int ldm_attention_ws(const ldm_attn_params* q, void* workspace, int64
   a.kvsplit = kv_splits(a, q->batch);
   const size_t rows = (size_t)q->batch * q->heads * q->n_q;
   a.opart = static_cast<float*>(workspace);
-  a.lsepart = a.opart + (size_t)a.kvsplit * rows * 40;
+  a.lsepart = a.opart + (size_t)a.kvsplit * rows * q->head_dim;
   return launch_kv_split(a, q->batch, s);
 }
 
