@@ -237,7 +237,7 @@ typedef struct {
 } ldm_attn_params;
 
 int ldm_attention(const ldm_attn_params* p, ldm_stream_t stream);
-/* As ldm_attention, with a caller workspace that lets the bf16 head_dim-40 / 80 paths split the keys
+/* As ldm_attention, with a caller workspace that lets the bf16 head_dim-40 / 80 / 160 paths split the keys
  * when the (batch, heads, n_q) grid alone would leave the GPU under-occupied (a single frame of the
  * 64x64 level: 128 eight-wave query blocks; of the 32x32 level: 32): each split writes a normalised fp32 partial and its
  * log-sum-exp to the workspace and a merge kernel combines them (same math, different fp32
@@ -266,6 +266,10 @@ void ldm_attention_force_legacy(int legacy);
 /* Tuning / A-B hook: 1 (default) runs head_dim 80 on the 32x32x16 kernel of head_dim 40, 0 on the
  * 16x16x32 one. */
 void ldm_attention_set_d80(int enabled);
+/* Tuning / A-B hook: 1 runs head_dim 160 on the 32x32x16 kernel of head_dim 40 (4 waves, 376
+ * registers per lane: one block per CU; split-KV through ldm_attention_ws), 0 (default: measured
+ * faster in the step) on the 16x16x32 one. */
+void ldm_attention_set_d160(int enabled);
 /* tuning / A-B hook: head_dim 40 with 64 queries per wave (two 32-query subtiles sharing every
  * K / V fragment read; 8 waves, one block per CU) */
 void ldm_attention_set_qs2(int enabled);

@@ -372,9 +372,13 @@ def test_attention_skew_bit_identical(B, N, hd):
     assert ((outs[1][0].float() - ref).norm() / ref.norm()).item() < 1e-2
 
 
-@pytest.mark.parametrize("B,N,splits", [(1, 4096, -1), (1, 4096 + 37, -1), (1, 64 * 5 + 3, 3), (1, 300, 2),
-                                         (2, 1024, 8), (1, 4096, 3), (1, 256 + 1, 2)])
-@pytest.mark.parametrize("hd", [40, 80])
+KVSPLIT_CASES = [(B, N, sp, hd) for hd in (40, 80) for B, N, sp in
+                 [(1, 4096, -1), (1, 4096 + 37, -1), (1, 64 * 5 + 3, 3), (1, 300, 2), (2, 1024, 8), (1, 4096, 3),
+                  (1, 256 + 1, 2)]] + [(1, 256, -1, 160), (1, 64, -1, 160), (1, 1024 + 5, 4, 160),
+                                       (2, 300, 2, 160), (8, 256, -1, 160)]
+
+
+@pytest.mark.parametrize("B,N,splits,hd", KVSPLIT_CASES)
 def test_attention_kvsplit(B, N, splits, hd):
     """ldm_attention_ws: head_dim 40 with the keys split over blocks (fp32 partials + log-sum-exp,
     merged by attn_kv_combine) against torch fp32 and against the unsplit kernel; a large logit sits
@@ -382,6 +386,7 @@ def test_attention_kvsplit(B, N, splits, hd):
     torch.manual_seed(12)
     H = 8
     C = H * hd
+    K.set_attention_d160(hd == 160)
     q, k, v = torch.randn(B, N, C), torch.randn(B, N, C), torch.randn(B, N, C)
     k[0, N - 2] = q[0, 5] * 4.0
     qkv = torch.cat([q, k, v], -1).to(DEV).to(torch.bfloat16)
@@ -391,10 +396,12 @@ def test_attention_kvsplit(B, N, splits, hd):
         K.set_attention_kvsplit(splits)
         p = K.AttnParams(0, 0, 0, 0, 3 * C, 3 * C, 3 * C, C, B, H, hd, N, N, hd ** -0.5, K.dtype_code(torch.bfloat16))
         p.q = p.k = p.v = p.o = 1 << 20              # any 16-byte-aligned address: sizing only
-        assert K.load_library().ldm_attention_workspace_bytes(ctypes.byref(p)) > 0
+        if N > 128:                                  # (N = 64: one key tile, never split)
+            assert K.load_library().ldm_attention_workspace_bytes(ctypes.byref(p)) > 0
         o1 = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C, 3 * C)
     finally:
         K.set_attention_kvsplit(-1)
+        K.set_attention_d160(False)
     x = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
     ref = (torch.softmax(x[0] @ x[1].transpose(-1, -2) * hd ** -0.5, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B, N, C)
     assert rel_err(o1, ref) < 1e-2
@@ -403,6 +410,32 @@ def test_attention_kvsplit(B, N, splits, hd):
     # one-pass kernel: the same bound as the qs2 form, and no worse against fp32 than the one pass
     assert (o1.float() - o0.float()).abs().max().item() < 0.05
     assert rel_err(o1, ref) <= 1.2 * rel_err(o0, ref) + 1e-4
+
+
+@pytest.mark.parametrize("B,N", [(8, 256), (1, 256), (8, 64), (2, 200)])
+def test_attention_d160_forms(B, N):
+    """head_dim 160 (the 16x16 / 8x8 levels) on the 32x32x16 kernel (ldm_attention_set_d160(True)) and
+    on the 16x16x32 one (default), both against torch fp32; unsplit (kvsplit 0)."""
+    torch.manual_seed(13)
+    H, hd = 8, 160
+    C = H * hd
+    qkv = torch.randn(B, N, 3 * C, device=DEV).to(torch.bfloat16)
+    x = qkv.float().view(B, N, 3, H, hd).permute(2, 0, 3, 1, 4)
+    ref = (torch.softmax(x[0] @ x[1].transpose(-1, -2) * hd ** -0.5, -1) @ x[2]).permute(0, 2, 1, 3).reshape(B, N, C)
+    outs = []
+    try:
+        K.set_attention_kvsplit(0)
+        for on in (True, False):
+            K.set_attention_d160(on)
+            o, lse = K.attention_fwd_lse(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C, 3 * C)
+            outs.append((o.float(), lse.float()))
+    finally:
+        K.set_attention_d160(False)
+        K.set_attention_kvsplit(-1)
+    for o, _ in outs:
+        assert ((o - ref).norm() / ref.norm()).item() < 1e-2
+    assert (outs[0][0] - outs[1][0]).abs().max().item() < 0.05
+    assert torch.allclose(outs[0][1], outs[1][1], atol=2e-2)
 
 
 def test_attention_kvsplit_planner():
@@ -418,7 +451,13 @@ def test_attention_kvsplit_planner():
     assert ws(8, 4096) == 0            # 1024 query blocks already
     assert ws(1, 1024, hd=80) > 0      # 32 eight-wave blocks at the 32x32 level
     assert ws(8, 1024, hd=80) == 0     # 256 already
-    assert ws(1, 256, hd=160) == 0
+    assert ws(1, 256, hd=160) == 0     # d = 160 stays on the 16x16x32 kernel by default
+    try:
+        K.set_attention_d160(True)
+        assert ws(1, 256, hd=160) > 0  # 16 four-wave blocks at the 16x16 level
+        assert ws(1, 64, hd=160) == 0  # the 8x8 level: one key tile
+    finally:
+        K.set_attention_d160(False)
     assert ws(1, 77) == 0              # a single key tile
     assert ws(4, 197) == 0             # 32 query blocks but only 4 key tiles
 

@@ -1380,20 +1380,22 @@ __global__ __launch_bounds__(256) void attn_kv_combine(const AttnArgs p) {
 }
 
 int g_attn_d80 = 1;      // tuning / A-B hook: 0 routes head_dim 80 to the 16x16x32 kernel
+int g_attn_d160 = 0;     // tuning / A-B hook: 1 routes head_dim 160 to the 32x32x16 kernel (measured slower:
+                         // B = 8 step 9.290 -> 9.373 ms, B = 1 4.180 -> 4.216, profiles/ab_r06/d160_*.json)
 int g_attn_kvsplit = -1;   // tuning / A-B hook (ldm_attention_set_kvsplit): -1 planner, 0 off, k >= 2 forced
 
 // split count: head_dim 40 — enough (query block, split) 8-wave blocks for two per CU, >= 4 key
 // tiles per split; head_dim 80 (one 8-wave block per CU) — 256 blocks, >= 2 key tiles per split;
 // 1 = no split
 int kv_splits(const AttnArgs& a, int batch) {
-  if (g_attn_kvsplit == 0 || !(a.d == 40 || (a.d == 80 && g_attn_d80))) return 1;
-  const int nblk = (a.nq + 255) / 256 * a.heads * batch;
+  if (g_attn_kvsplit == 0 || !(a.d == 40 || (a.d == 80 && g_attn_d80) || (a.d == 160 && g_attn_d160))) return 1;
+  const int nblk = (a.nq + (a.d == 160 ? 127 : 255)) / (a.d == 160 ? 128 : 256) * a.heads * batch;
   const int target = a.d == 40 ? 512 : 256;
   const int ntiles = (a.nkv + 63) / 64;
   int sp = g_attn_kvsplit > 0 ? g_attn_kvsplit : (nblk >= target ? 1 : (target + nblk - 1) / nblk);
   // the planner keeps >= 4 key tiles per split at d = 40 (a short sequence is launch-bound: the
   // merge kernel would cost more than the occupancy buys); forced splits go down to 2 tiles
-  sp = min(sp, min(8, ntiles / (g_attn_kvsplit > 0 || a.d == 80 ? 2 : 4)));
+  sp = min(sp, min(8, ntiles / (g_attn_kvsplit > 0 || a.d != 40 ? 2 : 4)));
   return sp >= 2 ? sp : 1;
 }
 
@@ -1412,6 +1414,11 @@ int launch_kv_split(const AttnArgs& a, int batch, hipStream_t s) {
     hipLaunchKernelGGL((attn_d40_kernel<8, 2, 64, 40, 1, false, true>), dim3(nblk), dim3(512), 0, s, a);
     LDM_CHECK_LAUNCH();
     hipLaunchKernelGGL((attn_kv_combine<40>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  } else if (a.d == 160) {
+    const int nb4 = (a.nq + 127) / 128 * a.heads * batch * a.kvsplit;
+    hipLaunchKernelGGL((attn_d40_kernel<4, 1, 64, 160, 1, false, true>), dim3(nb4), dim3(256), 0, s, a);
+    LDM_CHECK_LAUNCH();
+    hipLaunchKernelGGL((attn_kv_combine<160>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
   } else {
     hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80, 1, false, true>), dim3(nblk), dim3(512), 0, s, a);
     LDM_CHECK_LAUNCH();
@@ -1427,6 +1434,16 @@ int g_attn_qs2 = 0;      // tuning / A-B hook: head_dim 40 as 64 queries per wav
 
 template <int DP, bool F8 = false>
 int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
+  if constexpr (DP == 160) {
+    if (!F8 && g_attn_d160 && a.d == 160) {
+      // the 32x32x16 form at head_dim 160 (the 16x16 / 8x8 levels): 4 waves x 32 queries, one block
+      // per CU (376 registers per lane, 100 KB of K / V tiles)
+      hipLaunchKernelGGL((attn_d40_kernel<4, 1, 64, 160>), dim3((a.nq + 127) / 128 * a.heads * batch), dim3(256), 0, s,
+                         a);
+      LDM_CHECK_LAUNCH();
+      return LDM_OK;
+    }
+  }
   if constexpr (DP == 80) {
     if (!F8 && g_attn_d80 && a.d == 80) {
       // the 32x32x16 form at head_dim 80 (the 32x32 level): 8 waves x 32 queries per block
@@ -2710,6 +2727,7 @@ extern "C" void ldm_attention_set_waves(int waves) { g_attn_waves = (waves == 4 
 
 extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy; }
 extern "C" void ldm_attention_set_d80(int enabled) { g_attn_d80 = enabled ? 1 : 0; }
+extern "C" void ldm_attention_set_d160(int enabled) { g_attn_d160 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_qs2(int mode) { g_attn_qs2 = mode == 1 || mode == 2 ? mode : 0; }
 extern "C" void ldm_attention_set_skew(int mode) { g_attn_skew = mode >= 1 && mode <= 3 ? mode : 0; }
 extern "C" void ldm_attention_set_bwd32(int enabled) { g_attn_bwd32 = enabled ? 1 : 0; }

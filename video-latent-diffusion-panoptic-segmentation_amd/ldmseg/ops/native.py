@@ -122,6 +122,7 @@ EXPORTS = {
     "ldm_attention_set_d80": (None, [_i]),
     "ldm_attention_set_qs2": (None, [_i]),
     "ldm_attention_set_skew": (None, [_i]),
+    "ldm_attention_set_d160": (None, [_i]),
     "ldm_attention_set_bwd32": (None, [_i]),
     "ldm_conv2d_wgrad_set_ring": (None, [_i]),
     "ldm_conv2d_wgrad_set_fast_loader": (None, [_i]),
@@ -675,6 +676,11 @@ def set_attention_skew(mode=0):
     """Tuning / A-B hook for head_dim 40 / 80 on the 32x32x16 kernel: 0 planner, 1 off, 2 the block's
     waves in two phases half an iteration apart (bit-identical)."""
     load_library().ldm_attention_set_skew(int(mode))
+
+
+def set_attention_d160(enabled=False):
+    """Tuning / A-B hook: head_dim 160 on the 32x32x16 kernel, or (default) the 16x16x32 one."""
+    load_library().ldm_attention_set_d160(1 if enabled else 0)
 
 
 def set_attention_kvsplit(splits=-1):
