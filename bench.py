@@ -71,8 +71,7 @@ def roofline(unet, stepper, ts, nsteps, dtype, fp8=False):
     try:
         for i in range(nsteps):
             t = ts[i % len(ts)]
-            stepper.t_int.copy_(stepper._ar[t:t + 1])
-            stepper.t_f.copy_(stepper._arf[t:t + 1])
+            stepper._tb.copy_(stepper._tab[t])
             stepper._body()
     finally:
         K.set_profiler(None)

@@ -699,14 +699,17 @@ class UNet(nn.Module):
             return self._forward_sources(sources, timestep, encoder_hidden_states)
 
     @torch.no_grad()
-    def forward_ddim_step(self, sources, timestep, scheduler, t_int, sample, encoder_hidden_states=None):
+    def forward_ddim_step(self, sources, timestep, scheduler, t_int, sample, encoder_hidden_states=None,
+                          prev_out=None):
         """One sampler step, trainers_ldm_cond.py:1144-1162: eps = unet(cat(sources), t) and
         scheduler.step(eps, t, sample) -> (prev_sample, pred_original_sample).  On the bf16 path the
         step runs inside the UNet tail's launch (ldm_unet_tail: GroupNorm -> SiLU -> conv_out -> DDIM
         on the same device arithmetic as ldm_ddim_step, the model output rounded to bf16 first, as the
-        unfused conv stores it); otherwise the two calls."""
+        unfused conv stores it); otherwise the two calls.  prev_out (fused path only): the tensor
+        prev_sample is written to — the sampler passes the latent buffer itself (an in-place update).
+        Callers must use the returned prev_sample, which is a new tensor on the unfused path."""
         s0 = sources[0]
-        ddim = scheduler.fused_step_args(t_int, sample, self.compute_dtype)
+        ddim = scheduler.fused_step_args(t_int, sample, self.compute_dtype, prev_out=prev_out)
         with K.gn_arena(("unet", id(self), tuple(s0.shape), self.compute_dtype), s0.device):
             r = self._forward_sources(sources, timestep, encoder_hidden_states, ddim=ddim)
         if isinstance(r, tuple):

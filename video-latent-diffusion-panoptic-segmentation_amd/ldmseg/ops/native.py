@@ -1101,7 +1101,12 @@ def unet_tail(x, batch, h, w, groups, gamma, beta, eps, pc: PackedConv, eps_dtyp
         _contig(smp, "sample")
         if smp.shape != (batch, pc.n, h, w) or d["t"].dtype != torch.int64 or d["t"].numel() != 1:
             raise ValueError("ddim sample must be NCHW [batch, cout, h, w] and t one int64 device element")
-        prev = torch.empty(smp.shape, dtype=d["out_dtype"], device=x.device)
+        prev = d.get("prev_out")
+        if prev is None:
+            prev = torch.empty(smp.shape, dtype=d["out_dtype"], device=x.device)
+        elif prev.shape != smp.shape or prev.dtype != d["out_dtype"] or not prev.is_contiguous():
+            raise ValueError("ddim prev_out must be a contiguous tensor of the sample's shape and the output dtype")
+        # (prev_out may be the sample itself: every element is read and written by the same thread)
         x0 = torch.empty(smp.shape, dtype=d["out_dtype"], device=x.device)
     p = UnetTailParams(_ptr(x), batch, h, w, c, _ptr(st), unit, slots, groups, float(eps), _ptr(gamma), _ptr(beta),
                        _ptr(pc.w), pc.kpad, pc.n, _ptr(pc.bias), _ptr(eps_out), dtype_code(eps_dtype),

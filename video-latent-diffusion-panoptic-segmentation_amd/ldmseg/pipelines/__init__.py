@@ -26,11 +26,16 @@ class DenoiseStep:
         self.rgb = rgb_latents.contiguous()
         self.lat = torch.zeros(B, 4, L, Lw, dtype=torch.float32, device=dev)
         self.cond = torch.zeros_like(self.rgb) if self_condition else None
-        self.t_int = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.t_f = torch.zeros(1, dtype=torch.float32, device=dev)
+        # the timestep as int64 (DDIM) and float32 (time embedding) in one 16-byte buffer, so one copy
+        # from a per-timestep device table sets both before a replay
+        self._tb = torch.zeros(16, dtype=torch.uint8, device=dev)
+        self.t_int = self._tb[0:8].view(torch.int64)
+        self.t_f = self._tb[8:12].view(torch.float32)
         ac, ar = scheduler._tables(dev)
-        self._ar = ar
-        self._arf = ar.to(torch.float32)
+        tab = torch.zeros(ar.numel(), 16, dtype=torch.uint8, device=dev)
+        tab[:, 0:8] = ar.to(torch.int64).view(-1, 1).view(torch.uint8)
+        tab[:, 8:12] = ar.to(torch.float32).view(-1, 1).view(torch.uint8)
+        self._tab = tab
         self.graph = None
         self.prev = self.x0 = None
         unet.prepare()
@@ -49,7 +54,8 @@ class DenoiseStep:
         srcs = [self.lat, self.rgb] + ([self.cond] if self.cond is not None else [])   # conv_in gather casts
         if hasattr(self.unet, "forward_ddim_step"):
             # UNet + scheduler.step, the step fused into the UNet tail's launch where it can be
-            return self.unet.forward_ddim_step(srcs, self.t_f, self.sched, self.t_int, self.lat)
+            # prev_sample written over the latents in place (the tail reads each element first)
+            return self.unet.forward_ddim_step(srcs, self.t_f, self.sched, self.t_int, self.lat, prev_out=self.lat)
         eps = self.unet.forward_sources(srcs, self.t_f)
         r = self.sched.step(eps, self.t_int, self.lat)
         return r.prev_sample, r.pred_original_sample
@@ -60,8 +66,7 @@ class DenoiseStep:
             self.cond.zero_()
 
     def run(self, t: int, last: bool):
-        self.t_int.copy_(self._ar[t:t + 1])
-        self.t_f.copy_(self._arf[t:t + 1])
+        self._tb.copy_(self._tab[t])
         if self.graph is not None:
             self.graph.replay()
             prev, x0 = self.prev, self.x0
@@ -71,7 +76,8 @@ class DenoiseStep:
             self.cond.copy_(x0)
         if last:
             return x0
-        self.lat.copy_(prev)
+        if prev.data_ptr() != self.lat.data_ptr():
+            self.lat.copy_(prev)
         return self.lat
 
 

@@ -139,10 +139,12 @@ class DDIMNoiseScheduler(object):
                                use_clipped_model_output, out_dtype)
         return DDIMNoiseSchedulerOutput(prev_sample=prev, pred_original_sample=x0)
 
-    def fused_step_args(self, timestep, sample: torch.FloatTensor, model_output_dtype, use_clipped_model_output=False):
+    def fused_step_args(self, timestep, sample: torch.FloatTensor, model_output_dtype, use_clipped_model_output=False,
+                        prev_out=None):
         """The step() arguments as the device-side dict a producer kernel that fuses the step takes
         (ldm_unet_tail: the UNet's conv_out epilogue runs this same arithmetic on its output), or None
-        when this configuration has no fused form."""
+        when this configuration has no fused form.  prev_out: where prev_sample goes (may be sample
+        itself, updated in place)."""
         if self.thresholding or self.prediction_type not in K.PRED:
             return None
         dev = sample.device
@@ -152,7 +154,7 @@ class DDIMNoiseScheduler(object):
                     step_ratio=self.num_train_timesteps // self.num_inference_steps,
                     prediction_type=self.prediction_type, clip_sample=self.clip_sample,
                     clip_range=self.clip_sample_range, use_clipped=use_clipped_model_output,
-                    out_dtype=torch.promote_types(model_output_dtype, sample.dtype))
+                    out_dtype=torch.promote_types(model_output_dtype, sample.dtype), prev_out=prev_out)
 
     def add_noise(self, original_samples: torch.FloatTensor, noise: torch.FloatTensor, timesteps: torch.IntTensor,
                   scale: float = 1.0, mask_noise_perc: Optional[float] = None) -> torch.FloatTensor:
