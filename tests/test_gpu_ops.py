@@ -462,6 +462,33 @@ def test_attention_kvsplit_planner():
     assert ws(4, 197) == 0             # 32 query blocks but only 4 key tiles
 
 
+@pytest.mark.parametrize("B,N,hd,splits", [(8, 4096, 40, 0), (4, 64 * 7 + 5, 40, 0), (8, 1024, 80, 0), (2, 1024 + 9, 80, 0),
+                                            (1, 4096, 40, -1), (1, 64 * 9 + 3, 40, 3), (1, 1024, 80, -1)])
+def test_attention_pair_bit_identical(B, N, hd, splits):
+    """ldm_attention_set_pair(1) (the head_dim-80 default): the key-tile loop unrolled by two runs the
+    same operations in the same order, so output and log-sum-exp are bit-identical to the one-tile
+    loop (odd and even tile counts, ragged tails; at head_dim 40 both settings run one kernel)."""
+    torch.manual_seed(14)
+    H = 8
+    C = H * hd
+    qkv = torch.randn(B, N, 3 * C, device=DEV).to(torch.bfloat16)
+    outs = []
+    try:
+        K.set_attention_kvsplit(splits)
+        for on in (False, True):
+            K.set_attention_pair(on)
+            outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C, 3 * C))
+            if splits == 0:
+                outs.append(K.attention_fwd_lse(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C,
+                                                3 * C)[1])
+    finally:
+        K.set_attention_pair(True)
+        K.set_attention_kvsplit(-1)
+    half = len(outs) // 2
+    for a, b in zip(outs[:half], outs[half:]):
+        assert torch.equal(a, b)
+
+
 def test_attention_softmax_spike():
     """Force the online-softmax rescale: a huge logit in the LAST kv tile of some rows."""
     torch.manual_seed(4)

@@ -50,13 +50,15 @@ def mm_case(M, K, N):
     return (lambda: torch.mm(a, b)), 2.0 * M * K * N, None
 
 
-def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True, d80=True, qs2=0, skew=0):
+def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True, d80=True, qs2=0, skew=0,
+              pair=True):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
     def run():
         K.set_attention_d80(d80)
         K.set_attention_qs2(qs2)
         K.set_attention_skew(skew)
+        K.set_attention_pair(pair)
         K.force_attention_legacy(legacy)
         K.set_attention_waves(waves)
         K.set_attention_maxcol(maxcol)
@@ -370,6 +372,8 @@ CASES = {
     "attn_4096_d40_fp8": lambda: attn_case(8, 4096, 320, fp8=True),
     "attn_4096_d40_qs2": lambda: attn_case(8, 4096, 320, qs2=1),
     "attn_4096_d40_noskew": lambda: attn_case(8, 4096, 320, skew=1),
+    "attn_1024_d80_nopair": lambda: attn_case(8, 1024, 640, pair=False),
+    "attn_1024_d80": lambda: attn_case(8, 1024, 640),
     "attn_4096_d40_skew": lambda: attn_case(8, 4096, 320, skew=2),
     "attn_4096_d40_occ1": lambda: attn_case(8, 4096, 320, skew=3),
     "attn_1024_d80_noskew": lambda: attn_case(8, 1024, 640, skew=1),

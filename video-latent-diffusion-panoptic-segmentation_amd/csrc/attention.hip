@@ -696,8 +696,16 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 // KVS: split-KV (config 2's single frame: 256 four-wave blocks left one wave per SIMD): block id =
 // (query block, split); the split walks key tiles [t0, t1) and writes its normalised fp32 output and
 // log-sum-exp, which attn_kv_combine merges
-template <int NW, int OCC, int KT = 64, int D = 40, int QS = 1, bool SKEW = false, bool KVS = false>
-__global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p) {
+// PAIR: the tile loop unrolled by two, so each tile's K / V buffer is a compile-time constant (LDS
+// fragment addresses as immediate offsets instead of a per-tile select + multiply-add) and the first
+// tile of a pair issues its successor without the ragged-tile test
+template <int V>
+struct IntC {
+  static constexpr int value = V;
+};
+template <int NW, int OCC, int KT = 64, int D = 40, int QS = 1, bool SKEW = false, bool KVS = false,
+          bool PAIR = false>
+__global__ __launch_bounds__(64 * NW, PAIR ? (OCC * NW + 3) / 4 : OCC) void attn_d40_kernel(const AttnArgs p) {
   typedef bf16_t T;
   typedef __attribute__((ext_vector_type(16))) float f32x16_t;
   static_assert(D % 8 == 0, "head dim");
@@ -780,6 +788,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
     kstep[s2] = dat ? (int64_t)KT * p.ks * ES : 0;
     vstep[s2] = dat ? (int64_t)KT * p.vs * ES : 0;
   }
+  unsigned soff[NSL];                // slot LDS offsets, wave-uniform (SGPRs, once)
+#pragma unroll
+  for (int s2 = 0; s2 < NSL; ++s2) soff[s2] = __builtin_amdgcn_readfirstlane((wave + NW * s2) * 64 * 16);
   auto issue_full = [&](int buf) {   // the next full tile (tile 1, 2, ... in order)
     const unsigned kb = lds0 + (unsigned)(buf * 2 * TILE * ES);
     const unsigned vb = kb + TILE * ES;
@@ -787,7 +798,7 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
     for (int s2 = 0; s2 < NSL; ++s2) {
       const int i = wave + NW * s2;
       if (i >= RCH * (KT / 64)) break;
-      const unsigned off = __builtin_amdgcn_readfirstlane(i * 64 * 16);
+      const unsigned off = soff[s2];
       glds16(kq[s2], kb + off);
       glds16(vq[s2], vb + off);
       kq[s2] += kstep[s2];
@@ -950,7 +961,25 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn_d40_kernel(const AttnArgs p
   issue_tile(t0 * KT, bufi(t0));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (!SKEW) {
+  if constexpr (!SKEW && PAIR) {
+    // tile t in buffer BQ; SURE: tile t + 1 is known to be a full tile
+    auto step = [&](int t, auto bq, auto sure) {
+      constexpr int BQ = decltype(bq)::value;
+      if (decltype(sure)::value || t + 1 < nfull) issue_full(BQ ^ 1);
+      else if (t + 1 < ntiles) issue_tile((t + 1) * KT, BQ ^ 1);
+#pragma unroll
+      for (int hf = 0; hf < KT / 64; ++hf) compute(BQ, t * KT, false, t == t0, hf);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    };
+    int t = t0;
+    if ((t & 1) && t < nfull) step(t++, IntC<1>{}, IntC<0>{});
+    for (; t + 1 < nfull; t += 2) {
+      step(t, IntC<0>{}, IntC<1>{});
+      step(t + 1, IntC<1>{}, IntC<0>{});
+    }
+    if (t < nfull) step(t, IntC<0>{}, IntC<0>{});
+  } else if constexpr (!SKEW) {
     for (int t = t0; t < nfull; ++t) {
       issue_next(t);
 #pragma unroll
@@ -1382,6 +1411,9 @@ __global__ __launch_bounds__(256) void attn_kv_combine(const AttnArgs p) {
 int g_attn_d80 = 1;      // tuning / A-B hook: 0 routes head_dim 80 to the 16x16x32 kernel
 int g_attn_d160 = 0;     // tuning / A-B hook: 1 routes head_dim 160 to the 32x32x16 kernel (measured slower:
                          // B = 8 step 9.290 -> 9.373 ms, B = 1 4.180 -> 4.216, profiles/ab_r06/d160_*.json)
+int g_attn_pair = 1;      // tuning / A-B hook (ldm_attention_set_pair): head_dim 80's two-tile unrolled loop
+                         // (31.4 -> 30.5 us; at head_dim 40 it needed 5 spilled VGPRs to keep two blocks
+                         // per CU: 222.0 -> 220.7 us, the step unchanged — not instantiated)
 int g_attn_kvsplit = -1;   // tuning / A-B hook (ldm_attention_set_kvsplit): -1 planner, 0 off, k >= 2 forced
 
 // split count: head_dim 40 — enough (query block, split) 8-wave blocks for two per CU, >= 4 key
@@ -1450,6 +1482,8 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
       const int nb8 = (a.nq + 255) / 256 * a.heads * batch;
       if (nb8 >= 256 && g_attn_skew == 2)
         hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80, 1, true>), dim3(nb8), dim3(512), 0, s, a);
+      else if (nb8 >= 256 && g_attn_pair)
+        hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80, 1, false, false, true>), dim3(nb8), dim3(512), 0, s, a);
       else if (nb8 >= 256) hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80>), dim3(nb8), dim3(512), 0, s, a);
       else hipLaunchKernelGGL((attn_d40_kernel<4, 2, 64, 80>), dim3((a.nq + 127) / 128 * a.heads * batch),
                               dim3(256), 0, s, a);
@@ -2696,6 +2730,8 @@ extern "C" int ldm_attention_ws(const ldm_attn_params* q, void* workspace, int64
   a.lsepart = a.opart + (size_t)a.kvsplit * rows * q->head_dim;
   return launch_kv_split(a, q->batch, s);
 }
+
+extern "C" void ldm_attention_set_pair(int enabled) { g_attn_pair = enabled ? 1 : 0; }
 
 extern "C" void ldm_attention_set_kvsplit(int splits) { g_attn_kvsplit = splits < 0 ? -1 : (splits == 1 ? 0 : splits); }
 

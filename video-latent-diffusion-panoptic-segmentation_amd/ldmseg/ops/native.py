@@ -100,6 +100,7 @@ EXPORTS = {
     "ldm_attention_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_ws": (_i, [ctypes.POINTER(AttnParams), _vp, _i64, _vp]),
     "ldm_attention_set_kvsplit": (None, [_i]),
+    "ldm_attention_set_pair": (None, [_i]),
     "ldm_attention_fp8_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(AttnParams)]),
     "ldm_attention_set_fp8_scaled": (None, [_i]),
     "ldm_attention_set_maxcol": (None, [_i]),
@@ -681,6 +682,11 @@ def set_attention_skew(mode=0):
 def set_attention_d160(enabled=False):
     """Tuning / A-B hook: head_dim 160 on the 32x32x16 kernel, or (default) the 16x16x32 one."""
     load_library().ldm_attention_set_d160(1 if enabled else 0)
+
+
+def set_attention_pair(enabled=True):
+    """Tuning / A-B hook: the head_dim 80 kernel's key-tile loop unrolled by two (default; bit-identical)."""
+    load_library().ldm_attention_set_pair(1 if enabled else 0)
 
 
 def set_attention_kvsplit(splits=-1):
