@@ -1417,12 +1417,13 @@ int g_attn_pair = 1;      // tuning / A-B hook (ldm_attention_set_pair): head_di
 int g_attn_kvsplit = -1;   // tuning / A-B hook (ldm_attention_set_kvsplit): -1 planner, 0 off, k >= 2 forced
 
 // split count: head_dim 40 — enough (query block, split) 8-wave blocks for two per CU, >= 4 key
-// tiles per split; head_dim 80 (one 8-wave block per CU) — 256 blocks, >= 2 key tiles per split;
-// 1 = no split
+// tiles per split; head_dim 80 (one 8-wave block per CU) — 128 blocks, >= 2 key tiles per split
+// (config 2's 32x32 level: 4 splits of 4 tiles measured 9 us per step faster than 8 of 2, the merge
+// traffic halved: profiles/ab_r06/kvsplit_counts_b1.json); 1 = no split
 int kv_splits(const AttnArgs& a, int batch) {
   if (g_attn_kvsplit == 0 || !(a.d == 40 || (a.d == 80 && g_attn_d80) || (a.d == 160 && g_attn_d160))) return 1;
   const int nblk = (a.nq + (a.d == 160 ? 127 : 255)) / (a.d == 160 ? 128 : 256) * a.heads * batch;
-  const int target = a.d == 40 ? 512 : 256;
+  const int target = a.d == 40 ? 512 : (a.d == 80 ? 128 : 256);
   const int ntiles = (a.nkv + 63) / 64;
   int sp = g_attn_kvsplit > 0 ? g_attn_kvsplit : (nblk >= target ? 1 : (target + nblk - 1) / nblk);
   // the planner keeps >= 4 key tiles per split at d = 40 (a short sequence is launch-bound: the
