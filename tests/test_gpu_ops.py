@@ -372,10 +372,11 @@ def test_attention_skew_bit_identical(B, N, hd):
     assert ((outs[1][0].float() - ref).norm() / ref.norm()).item() < 1e-2
 
 
-KVSPLIT_CASES = [(B, N, sp, hd) for hd in (40, 80) for B, N, sp in
-                 [(1, 4096, -1), (1, 4096 + 37, -1), (1, 64 * 5 + 3, 3), (1, 300, 2), (2, 1024, 8), (1, 4096, 3),
-                  (1, 256 + 1, 2)]] + [(1, 256, -1, 160), (1, 64, -1, 160), (1, 1024 + 5, 4, 160),
-                                       (2, 300, 2, 160), (8, 256, -1, 160)]
+# planner cases at each head dim's UNet level (d = 40: 64x64, N = 4096; d = 80: 32x32, N = 1024)
+KVSPLIT_CASES = [(B, N * (4 if hd == 40 else 1) + r, sp, hd) for hd in (40, 80) for B, N, r, sp in
+                 [(1, 1024, 0, -1), (1, 1024, 37, -1), (1, 0, 64 * 5 + 3, 3), (1, 0, 300, 2), (2, 0, 1024, 8),
+                  (1, 1024, 0, 3), (1, 0, 256 + 1, 2)]] + [(1, 256, -1, 160), (1, 64, -1, 160), (1, 1024 + 5, 4, 160),
+                                                          (2, 300, 2, 160), (8, 256, -1, 160)]
 
 
 @pytest.mark.parametrize("B,N,splits,hd", KVSPLIT_CASES)
