@@ -239,7 +239,8 @@ typedef struct {
 int ldm_attention(const ldm_attn_params* p, ldm_stream_t stream);
 /* As ldm_attention, with a caller workspace that lets the bf16 head_dim-40 / 80 / 160 paths split the keys
  * when the (batch, heads, n_q) grid alone would leave the GPU under-occupied (a single frame of the
- * 64x64 level: 128 eight-wave query blocks; of the 32x32 level: 32): each split writes a normalised fp32 partial and its
+ * 64x64 level: 128 eight-wave query blocks; of the 32x32 level: 32; of the 16x16 level: 32 four-wave
+ * blocks of the 16x16x32 head_dim-160 kernel): each split writes a normalised fp32 partial and its
  * log-sum-exp to the workspace and a merge kernel combines them (same math, different fp32
  * summation order).  ldm_attention_workspace_bytes returns 0 when no split applies; then the call
  * is exactly ldm_attention and the workspace may be NULL. */

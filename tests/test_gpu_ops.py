@@ -376,18 +376,20 @@ def test_attention_skew_bit_identical(B, N, hd):
 KVSPLIT_CASES = [(B, N * (4 if hd == 40 else 1) + r, sp, hd) for hd in (40, 80) for B, N, r, sp in
                  [(1, 1024, 0, -1), (1, 1024, 37, -1), (1, 0, 64 * 5 + 3, 3), (1, 0, 300, 2), (2, 0, 1024, 8),
                   (1, 1024, 0, 3), (1, 0, 256 + 1, 2)]] + [(1, 256, -1, 160), (1, 64, -1, 160), (1, 1024 + 5, 4, 160),
-                                                          (2, 300, 2, 160), (8, 256, -1, 160)]
+                                                          (2, 300, 2, 160), (8, 256, -1, 160), (1, 200, 4, 160)]
+# head_dim 160 runs on the 16x16x32 kernel by default and on the 32x32x16 one under ldm_attention_set_d160
+KVSPLIT_CASES = [c + (False,) for c in KVSPLIT_CASES] + [c + (True,) for c in KVSPLIT_CASES if c[3] == 160]
 
 
-@pytest.mark.parametrize("B,N,splits,hd", KVSPLIT_CASES)
-def test_attention_kvsplit(B, N, splits, hd):
+@pytest.mark.parametrize("B,N,splits,hd,route32", KVSPLIT_CASES)
+def test_attention_kvsplit(B, N, splits, hd, route32):
     """ldm_attention_ws: head_dim 40 with the keys split over blocks (fp32 partials + log-sum-exp,
     merged by attn_kv_combine) against torch fp32 and against the unsplit kernel; a large logit sits
     in the last key tile so the merge's rescale is exercised."""
     torch.manual_seed(12)
     H = 8
     C = H * hd
-    K.set_attention_d160(hd == 160)
+    K.set_attention_d160(route32)
     q, k, v = torch.randn(B, N, C), torch.randn(B, N, C), torch.randn(B, N, C)
     k[0, N - 2] = q[0, 5] * 4.0
     qkv = torch.cat([q, k, v], -1).to(DEV).to(torch.bfloat16)
@@ -397,7 +399,7 @@ def test_attention_kvsplit(B, N, splits, hd):
         K.set_attention_kvsplit(splits)
         p = K.AttnParams(0, 0, 0, 0, 3 * C, 3 * C, 3 * C, C, B, H, hd, N, N, hd ** -0.5, K.dtype_code(torch.bfloat16))
         p.q = p.k = p.v = p.o = 1 << 20              # any 16-byte-aligned address: sizing only
-        if N > 128:                                  # (N = 64: one key tile, never split)
+        if N > 128 and not (B == 8 and hd == 160 and not route32):   # (N = 64: one key tile; B = 8 fills)
             assert K.load_library().ldm_attention_workspace_bytes(ctypes.byref(p)) > 0
         o1 = K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C, 3 * C)
     finally:
@@ -452,7 +454,9 @@ def test_attention_kvsplit_planner():
     assert ws(8, 4096) == 0            # 1024 query blocks already
     assert ws(1, 1024, hd=80) > 0      # 32 eight-wave blocks at the 32x32 level
     assert ws(8, 1024, hd=80) == 0     # 256 already
-    assert ws(1, 256, hd=160) == 0     # d = 160 stays on the 16x16x32 kernel by default
+    assert ws(1, 256, hd=160) > 0      # 32 four-wave blocks of the 16x16x32 kernel at the 16x16 level
+    assert ws(8, 256, hd=160) == 0     # 256 already
+    assert ws(1, 64, hd=160) == 0      # the 8x8 level: one key tile
     try:
         K.set_attention_d160(True)
         assert ws(1, 256, hd=160) > 0  # 16 four-wave blocks at the 16x16 level

@@ -368,7 +368,10 @@ __device__ __forceinline__ uint4 scale_bf16x8(uint4 v, float c) {
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <int DP, int QSUB, bool ONES, int NW = 4, int OCC = 8 / NW, bool F8 = false, bool MC = false>
+// KVS: split-KV as in attn_d40_kernel (block id = (query block, split), key tiles [t0, t1), fp32
+// partials + log-sum-exp for attn_kv_combine)
+template <int DP, int QSUB, bool ONES, int NW = 4, int OCC = 8 / NW, bool F8 = false, bool MC = false,
+          bool KVS = false>
 __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) {
   typedef bf16_t T;
   constexpr int ES = 2, EPC = 8;
@@ -389,18 +392,25 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
   // 1-D grid, XCD-aware: blocks b and b+8 share an XCD, so each XCD gets a contiguous run of
   // (batch, head, q-block) ids and the q-blocks of one head read its K/V from one L2 (with the
   // 3-D grid the 8 q-blocks of a head landed on 8 XCDs: 8x the K/V misses)
-  int qb, h, b;
+  int qb, h, b, split = 0;
   {
     const int nqb = (p.nq + 16 * QSUB * NW - 1) / (16 * QSUB * NW);
     const int bid = blockIdx.x, nblk = gridDim.x;
     const int xcd = bid & 7, qq = nblk >> 3, rem = nblk & 7;
-    const int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    int t = (xcd < rem ? xcd * (qq + 1) : rem * (qq + 1) + (xcd - rem) * qq) + (bid >> 3);
+    if constexpr (KVS) {
+      split = t % p.kvsplit;
+      t /= p.kvsplit;
+    }
     qb = t % nqb;
     const int hb = t / nqb;
     h = hb % p.heads;
     b = hb / p.heads;
   }
   const int qbase = qb * (16 * QSUB * NW) + wave * 16 * QSUB;
+  const int ntiles_all = (p.nkv + KVT - 1) / KVT;
+  const int t0 = KVS ? ntiles_all * split / p.kvsplit : 0;               // this block's key tiles
+  const int t1 = KVS ? ntiles_all * (split + 1) / p.kvsplit : ntiles_all;
 
   const T* qp = reinterpret_cast<const T*>(p.q) + (int64_t)b * p.nq * p.qs + (int64_t)h * p.d;
   const T* kp = reinterpret_cast<const T*>(p.k) + (int64_t)b * p.nkv * p.ks + (int64_t)h * p.d;
@@ -438,9 +448,9 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
     const bool dat = i < RCH && c < CPR && c * EPC < p.d;
     const bool kone = MC && c == p.d / EPC;
     const bool vone = c == ones_chunk;
-    kq[s2] = dat ? reinterpret_cast<const char*>(kp + (int64_t)(KVT + row) * p.ks + c * EPC)
+    kq[s2] = dat ? reinterpret_cast<const char*>(kp + (int64_t)((t0 + 1) * KVT + row) * p.ks + c * EPC)
                  : reinterpret_cast<const char*>(kone ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
-    vq[s2] = dat ? reinterpret_cast<const char*>(vp + (int64_t)(KVT + row) * p.vs + c * EPC)
+    vq[s2] = dat ? reinterpret_cast<const char*>(vp + (int64_t)((t0 + 1) * KVT + row) * p.vs + c * EPC)
                  : reinterpret_cast<const char*>(vone ? (const void*)&kOnesBf16 : (const void*)&kZeros16);
     kstep[s2] = dat ? (int64_t)KVT * p.ks * ES : 0;
     vstep[s2] = dat ? (int64_t)KVT * p.vs * ES : 0;
@@ -630,19 +640,20 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
 
   // full tiles in the loop (one compute body: no per-tile copies of the accumulators between
   // a masked and an unmasked instance), the ragged last tile after it
-  const int ntiles = (p.nkv + KVT - 1) / KVT;
-  const int nfull = p.nkv / KVT;
-  issue_tile(0, 0);
+  const int ntiles = t1;
+  const int nfull = KVS ? min(p.nkv / KVT, t1) : p.nkv / KVT;
+  issue_tile(t0 * KVT, t0 & 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int t = 0; t < nfull; ++t) {
+  for (int t = t0; t < nfull; ++t) {
     if (t + 1 < nfull) issue_full((t + 1) & 1);
     else if (t + 1 < ntiles) issue_tile((t + 1) * KVT, (t + 1) & 1);
-    compute(t & 1, t * KVT, false, t == 0);
+    compute(t & 1, t * KVT, false, t == t0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  if (nfull < ntiles) compute(nfull & 1, nfull * KVT, true, nfull == 0);
+  const int tr = KVS ? max(nfull, t0) : nfull;             // the ragged last tile
+  if (tr < ntiles) compute(tr & 1, tr * KVT, true, tr == t0);
 
   T* op = reinterpret_cast<T*>(p.o) + (int64_t)b * p.nq * p.os + (int64_t)h * p.d;
 #pragma unroll
@@ -657,6 +668,20 @@ __global__ __launch_bounds__(64 * NW, OCC) void attn32_kernel(const AttnArgs p) 
     const float inv = 1.0f / lt;
     const int qi = qbase + 16 * s + lr;
     if (qi >= p.nq) continue;
+    if constexpr (KVS) {
+      // this split's normalised output and log-sum-exp (fp32) for attn_kv_combine
+      const int64_t row = ((int64_t)split * p.batch + b) * p.heads * p.nq + (int64_t)h * p.nq + qi;
+      if (g == 0) p.lsepart[row] = mrun[s] + __log2f(lt);
+      float* orow = p.opart + row * p.d;
+#pragma unroll
+      for (int dd = 0; dd < ND; ++dd) {
+        const int d = 16 * dd + 4 * g;
+        if (d >= p.d) continue;
+        *reinterpret_cast<float4*>(orow + d) = make_float4(oacc[dd][s][0] * inv, oacc[dd][s][1] * inv,
+                                                           oacc[dd][s][2] * inv, oacc[dd][s][3] * inv);
+      }
+      continue;
+    }
     if (p.lse && g == 0) p.lse[((int64_t)b * p.heads + h) * p.nq + qi] = mrun[s] + __log2f(lt);
 #pragma unroll
     for (int dd = 0; dd < ND; ++dd) {
@@ -1421,14 +1446,20 @@ int g_attn_kvsplit = -1;   // tuning / A-B hook (ldm_attention_set_kvsplit): -1 
 // (config 2's 32x32 level: 4 splits of 4 tiles measured 9 us per step faster than 8 of 2, the merge
 // traffic halved: profiles/ab_r06/kvsplit_counts_b1.json); 1 = no split
 int kv_splits(const AttnArgs& a, int batch) {
-  if (g_attn_kvsplit == 0 || !(a.d == 40 || (a.d == 80 && g_attn_d80) || (a.d == 160 && g_attn_d160))) return 1;
-  const int nblk = (a.nq + (a.d == 160 ? 127 : 255)) / (a.d == 160 ? 128 : 256) * a.heads * batch;
+  if (g_attn_kvsplit == 0 || !(a.d == 40 || (a.d == 80 && g_attn_d80) || a.d == 160)) return 1;
+  // d = 160: the 32x32x16 route (hook) counts 128-query blocks, the default 16x16x32 kernel 64-query
+  // four-wave blocks (its 8-wave form when that gives >= 256 blocks: never split)
+  const int qpb = a.d == 160 ? (g_attn_d160 ? 128 : 64) : 256;
+  const int nblk = (a.nq + qpb - 1) / qpb * a.heads * batch;
+  if (a.d == 160 && !g_attn_d160 && (a.nq + 127) / 128 * a.heads * batch >= 256) return 1;
   const int target = a.d == 40 ? 512 : (a.d == 80 ? 128 : 256);
   const int ntiles = (a.nkv + 63) / 64;
   int sp = g_attn_kvsplit > 0 ? g_attn_kvsplit : (nblk >= target ? 1 : (target + nblk - 1) / nblk);
   // the planner keeps >= 4 key tiles per split at d = 40 (a short sequence is launch-bound: the
-  // merge kernel would cost more than the occupancy buys); forced splits go down to 2 tiles
-  sp = min(sp, min(8, ntiles / (g_attn_kvsplit > 0 || a.d != 40 ? 2 : 4)));
+  // merge kernel would cost more than the occupancy buys), >= 2 at d = 80 and on the d = 160
+  // 32x32x16 route; the 16x16x32 d = 160 kernel and forced splits go down to 1 / 2 tiles
+  const int mint = a.d == 160 && !g_attn_d160 ? 1 : (g_attn_kvsplit > 0 || a.d != 40 ? 2 : 4);
+  sp = min(sp, min(8, ntiles / mint));
   return sp >= 2 ? sp : 1;
 }
 
@@ -1447,6 +1478,11 @@ int launch_kv_split(const AttnArgs& a, int batch, hipStream_t s) {
     hipLaunchKernelGGL((attn_d40_kernel<8, 2, 64, 40, 1, false, true>), dim3(nblk), dim3(512), 0, s, a);
     LDM_CHECK_LAUNCH();
     hipLaunchKernelGGL((attn_kv_combine<40>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  } else if (a.d == 160 && !g_attn_d160) {
+    const int nb4 = (a.nq + 63) / 64 * a.heads * batch * a.kvsplit;
+    hipLaunchKernelGGL((attn32_kernel<160, 1, false, 4, 2, false, false, true>), dim3(nb4), dim3(256), 0, s, a);
+    LDM_CHECK_LAUNCH();
+    hipLaunchKernelGGL((attn_kv_combine<160>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
   } else if (a.d == 160) {
     const int nb4 = (a.nq + 127) / 128 * a.heads * batch * a.kvsplit;
     hipLaunchKernelGGL((attn_d40_kernel<4, 1, 64, 160, 1, false, true>), dim3(nb4), dim3(256), 0, s, a);
