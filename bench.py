@@ -117,7 +117,9 @@ def roofline(unet, stepper, ts, nsteps, dtype, fp8=False):
         achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9
         rl = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
               "frac": round(achieved / PEAK_HBM_GBS, 4)}
-    rl["traffic"], rl["traffic_source"] = pmc_traffic(dom)
+    rl["pmc_workload"] = pmc_key = f"B={unet_batch(stepper)} {stepper.lat.shape[-2]}x{stepper.lat.shape[-1]} " \
+        f"{str(dtype).replace('torch.', '')}{' fp8' if fp8 else ''}"
+    rl["traffic"], rl["traffic_source"] = pmc_traffic(dom, pmc_key)
     rl["avg_launch_ms"] = round(d["ms"] / d["launches"], 5)
     rl["launches_per_step"] = d["launches"] // nsteps
     rl["algorithmic_flops_per_launch"] = round(d["flops"] / d["launches"], 1)
@@ -126,16 +128,24 @@ def roofline(unet, stepper, ts, nsteps, dtype, fp8=False):
     return rl
 
 
-def pmc_traffic(family):
-    """HBM bytes per launch of `family` from the newest committed PMC summary
+def unet_batch(stepper):
+    return stepper.lat.shape[0]
+
+
+def pmc_traffic(family, workload):
+    """HBM bytes per launch of `family` from the newest committed PMC summary of the SAME workload
     (profiles/rNN_families.json, written by tools/profile_bench.sh from separate FETCH_SIZE /
-    WRITE_SIZE rocprofv3 passes over this same command).  A live bench run cannot read PMC
-    counters itself; None when no summary exists."""
+    WRITE_SIZE rocprofv3 passes over this same command, tagged with the bench line's
+    `pmc_workload`).  A live bench run cannot read PMC counters itself; None when no summary of
+    this workload exists (a B=1 or config-5 line never borrows the B=8 figure)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_families.json")))
     for f in reversed(files):
         try:
-            fam = json.load(open(f))["families"].get(family, {})
+            meta = json.load(open(f))
+            if meta.get("workload") != workload:
+                continue
+            fam = meta["families"].get(family, {})
         except (OSError, ValueError, KeyError):
             continue
         if "traffic_bytes_per_call" in fam:

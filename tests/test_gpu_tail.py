@@ -101,3 +101,44 @@ def test_unet_forward_ddim_step_fused_vs_unfused():
         u.set_tail_fused(True)
     assert p1.dtype == p2.dtype == torch.float32
     assert rel_err(p1, p2) < 2e-2 and rel_err(x1, x2) < 2e-2
+
+
+def _small_bf16_unet(cond_channels):
+    from ldmseg.models import UNet
+    torch.manual_seed(0)
+    u = UNet(block_out_channels=(64, 128, 128, 128), cross_attention_dim=None)
+    with torch.no_grad():
+        for _, p in u.named_parameters():
+            if p.ndim == 1:
+                p.add_(torch.randn_like(p) * 0.1)
+    u.modify_encoder(in_channels=8, init_mode_seg="copy", init_mode_image="random", cond_channels=cond_channels,
+                     init_mode_cond="random")
+    return u.eval().to(DEV, BF)
+
+
+@pytest.mark.parametrize("self_condition", [False, True])
+def test_sample_latents_bf16_inplace_tail(self_condition):
+    """The headline sampling path: DenoiseStep passes prev_out = its latents, so the fused
+    bf16 tail writes prev_sample over the latents it reads, inside the captured step graph; with
+    self-conditioning the x0 of each step is copied into the third conv_in source, and the last step
+    returns x0.  Graph replay must equal eager bit for bit, and both must match the unfused tail
+    (ldm_group_norm + ldm_conv2d + ldm_ddim_step into fresh tensors, then copied) within the tail's
+    bf16 bar at every step."""
+    from ldmseg.pipelines import sample_latents
+    from ldmseg.schedulers import DDIMNoiseScheduler
+    u = _small_bf16_unet(4 if self_condition else 0)
+    sch = DDIMNoiseScheduler()
+    g = torch.Generator(device=DEV).manual_seed(11)
+    rgb = torch.randn(2, 4, 32, 32, device=DEV, generator=g)
+    kw = dict(num_inference_steps=6, seed=3, self_condition=self_condition, return_all_latents=True)
+    eager = sample_latents(u, sch, rgb, use_graph=False, **kw)
+    graph = sample_latents(u, sch, rgb, use_graph=True, **kw)
+    assert eager.shape == (6 * 2, 4, 32, 32) and torch.isfinite(eager).all()
+    assert torch.equal(eager, graph)
+    u.set_tail_fused(False)
+    try:
+        unfused = sample_latents(u, sch, rgb, use_graph=False, **kw)
+    finally:
+        u.set_tail_fused(True)
+    for s in range(6):
+        assert rel_err(eager[2 * s:2 * s + 2], unfused[2 * s:2 * s + 2]) < 3e-2, s

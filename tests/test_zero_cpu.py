@@ -112,3 +112,43 @@ def test_zero1_shards_and_consolidated_state_world2(tmp_path):
     assert all(a[1] <= b[0] for a, b in zip(merged, merged[1:]))
     assert same0 and same1 and st0 == st1 == 1
     assert (d0 == d1).all()                         # rank 0's weights broadcast at construction
+
+
+def _subgroup_worker(rank, world, port, q, tmp):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from torch.distributed.optim import ZeroRedundancyOptimizer
+        from ldmseg.utils import checkpoint as ck
+        groups = [dist.new_group([r]) for r in range(world)]      # every rank creates every group
+        torch.manual_seed(rank)
+        lin = torch.nn.Linear(8, 8)
+        opt = ZeroRedundancyOptimizer(lin.parameters(), optimizer_class=torch.optim.AdamW, lr=1e-3,
+                                      process_group=groups[rank])
+        lin(torch.randn(4, 8)).square().sum().backward()
+        opt.step()
+        path = os.path.join(tmp, f"model_{rank}.pt")
+        ck.save(path, unet=lin, vae_semseg=torch.nn.Identity(), opt=opt)
+        sd = ck.read(path)["opt"] if os.path.exists(path) else None
+        q.put((rank, sd is not None and len(sd["state"]) == 2 and sd["state"][0]["step"].item() == 1))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_save_torch_zero_over_subgroup_without_rank0(tmp_path):
+    """a torch ZeroRedundancyOptimizer keeps its group in `process_group`.  Over a
+    subgroup that excludes global rank 0 the state is consolidated to that group's first rank, and
+    that rank (not global rank 0, which holds none of it) must write the file."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_subgroup_worker, args=(r, world, port, q, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == [(0, True), (1, True)]

@@ -26,23 +26,18 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# (family, regex on the kernel name, is_primary) — primary kernels count calls
-FAMILIES = [
-    ("igemm", r"(igemm_kernel|igemm_big_kernel|conv3_halo_kernel|gemm_ars2?_kernel|gemm_wide_kernel)<|feedforward_kernel|"
-              r"transformer_in_kernel", True),
-    ("igemm", r"splitk_epilogue_kernel<", False),
-    ("attention", r"attn(32|_d40|_f8)?_kernel<", True),
-    ("group_norm", r"gn_apply", True),
-    ("group_norm", r"gn_(partial|finalize)", False),
-    ("layer_norm", r"ln_kernel<", True),
-]
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kernel_families import kind_of  # noqa: E402  (the table shared with traffic_table / step_trace)
 
 
 def family_of(name):
-    for fam, rx, primary in FAMILIES:
-        if re.search(rx, name):
-            return fam, primary
-    return "other", True
+    """(family, is_primary): primary kernels count calls; others add time / traffic to their family."""
+    fam, role = kind_of(name)
+    if fam is None:
+        return "other", True
+    return fam, role == "p"
 
 
 def _one(pattern):
@@ -115,7 +110,8 @@ def main():
         for line in open(a.bench):
             if line.startswith("{"):
                 bench = json.loads(line)
-    meta = {"tag": a.tag, "command": "python3 bench.py (see tools/profile_bench.sh)",
+    workload = ((bench or {}).get("roofline") or {}).get("pmc_workload")
+    meta = {"tag": a.tag, "command": "python3 bench.py (see tools/profile_bench.sh)", "workload": workload,
             "traffic_method": "2*FETCH_SIZE + WRITE_SIZE (KiB->bytes), separate --pmc passes, eager steps",
             "families": result, "bench": bench}
     json.dump(meta, open(os.path.join(out_dir, f"{a.tag}_families.json"), "w"), indent=1)

@@ -21,24 +21,10 @@ import os
 import re
 from collections import defaultdict
 
-# (family, regex, role): role "p" primary, "post" attaches to the previous op, "pre" to the next
-KINDS = [
-    ("igemm", r"(igemm_kernel|igemm_big_kernel|conv3_halo_kernel|gemm_ars2?_kernel|gemm_wide_kernel)<|"
-              r"feedforward_kernel|transformer_in_kernel", "p"),
-    ("igemm", r"splitk_epilogue_kernel<", "post"),
-    ("attention", r"attn(32|_d40|_f8)?_kernel<", "p"),
-    ("attention", r"attn_f8_prep", "pre"),
-    ("group_norm", r"gn_apply|gn_small", "p"),
-    ("group_norm", r"gn_stats", "pre"),
-    ("layer_norm", r"ln_kernel<", "p"),
-]
+import sys
 
-
-def kind_of(name):
-    for fam, rx, role in KINDS:
-        if re.search(rx, name):
-            return fam, role
-    return None, None
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from kernel_families import kind_of  # noqa: E402  (the table shared with rocprof_summary / step_trace)
 
 
 def short(name):
@@ -76,6 +62,7 @@ def main():
     assign = {}
     oi = len(ops) - 1
     pending_post = []
+    first = None
     for did in reversed(disp):
         if oi < 0:
             break
@@ -89,13 +76,21 @@ def main():
             if oi + 1 < len(ops):
                 assign.setdefault(oi + 1, []).append(did)
             continue
-        while oi >= 0 and ops[oi]["family"] != fam:
-            oi -= 1
-        if oi < 0:
-            break
+        # strict alignment: the dispatch must be the op the log names next (walking back), so a
+        # kernel the family table does not know can never shift the kernel column against the ops
+        if ops[oi]["family"] != fam:
+            raise SystemExit(f"traffic_table: dispatch {did} ({short(meta[did][0])}, family {fam}) does not "
+                             f"match op {oi} ({ops[oi]['family']}: {ops[oi]['detail']}); "
+                             f"is a kernel missing from tools/kernel_families.py?")
         assign.setdefault(oi, []).extend([did] + pending_post)
         pending_post = []
+        first = did
         oi -= 1
+    if oi >= 0:
+        raise SystemExit(f"traffic_table: {oi + 1} ops of the log have no dispatch")
+    nprim = sum(1 for d in disp if d >= first and kind_of(meta[d][0])[1] == "p")
+    if nprim != len(ops):
+        raise SystemExit(f"traffic_table: {nprim} primary dispatches in the profiled step, {len(ops)} ops logged")
     rows = []
     for i, op in enumerate(ops):
         ds = assign.get(i)

@@ -896,6 +896,9 @@ __global__ __launch_bounds__(512, 1) void conv3_halo_kernel(const ConvArgs p) {
   constexpr int HW = G::HW, HPIX = G::HPIX, NP = G::NP, A_TAPS = G::A_TAPS, HALO_U4 = G::HALO_U4;
   constexpr int NBS = G::NBS;
   static_assert(A_TAPS <= 7, "halo geometry");
+  // the single counted vmcnt(1 + 4 * (NBS - 2)) wait assumes every halo piece of channel block cb + 1
+  // (issued over taps < A_TAPS of block cb) is older than B stage s at (cb + 1, tap 0)
+  static_assert(A_TAPS + NBS <= 10, "halo pieces must retire before the B ring's counted wait");
   constexpr int WT = BM / 4;                      // wave tile rows
   constexpr int FM = WT / 16, FN = 5;
   constexpr int EPI_H = BM > 128 ? 2 : 1;

@@ -284,7 +284,9 @@ extern "C" int ldm_unet_tail(const ldm_unet_tail_params* p, ldm_stream_t stream)
                (p->sample_dtype != LDM_F32 && p->sample_dtype != LDM_BF16)))
     return LDM_ERR_ARG;
   if ((reinterpret_cast<uintptr_t>(p->h) & 15) || (reinterpret_cast<uintptr_t>(p->w) & 15)) return LDM_ERR_ALIGN;
-  if ((int64_t)p->batch * p->height * p->width * p->c >= (1LL << 31) - 64) return LDM_ERR_ARG;   // int offsets
+  // the kernel works in int BYTE offsets with 0x7ffff000 as the zero-padding sentinel: the tensor's
+  // byte size must stay below the sentinel so offsets never wrap and the sentinel is always out of range
+  if ((int64_t)p->batch * p->height * p->width * p->c * 2 >= (1LL << 31) - 4096) return LDM_ERR_ARG;
   TailArgs a;
   a.h = static_cast<const bf16_t*>(p->h);
   a.batch = p->batch; a.H = p->height; a.W = p->width; a.C = p->c;

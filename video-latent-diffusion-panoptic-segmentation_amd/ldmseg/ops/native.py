@@ -1070,9 +1070,13 @@ def linear_rows(pc: PackedConv, x, rows, *, act=ACT_NONE, out_dtype=None, t=None
         raise ValueError("x must be [rows, cin]")
     out_dtype = out_dtype or pc.dtype
     out = torch.empty(rows, pc.n, dtype=out_dtype, device=dev)
+    ev = _prof_start()
     _check(lib.ldm_linear_rows(_ptr(x), _ptr(t), 0 if t is None else t.numel(), _ptr(freqs), int(flip_sin_to_cos),
                                _ptr(pc.w), pc.kpad, pc.cin, pc.n, _ptr(pc.bias), rows, act, _ptr(out),
                                dtype_code(out_dtype), _stream(pc.w)), "ldm_linear_rows")
+    _prof_stop(ev, "linear_rows", 2.0 * rows * pc.n * pc.cin_real, pc.w.numel() * pc.w.element_size() +
+               rows * (pc.cin * (0 if x is None else x.element_size()) + pc.n * out.element_size()),
+               f"rows={rows} N={pc.n} K={pc.cin_real}")
     return out
 
 

@@ -67,7 +67,8 @@ def save(path, **kw):
         # consolidate onto the writer: `to` is a rank of the optimizer's own process group, so map
         # global rank 0 into it; a group without global rank 0 consolidates to (and is written by)
         # its own first rank
-        to, group = 0, getattr(opt, "group", None)
+        # (LDMTrainStep keeps its group in `group`, torch ZeroRedundancyOptimizer in `process_group`)
+        to, group = 0, getattr(opt, "group", None) or getattr(opt, "process_group", None)
         if dist_on and group is not None:
             try:
                 to = dist.get_group_rank(group, 0)
