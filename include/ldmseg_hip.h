@@ -107,6 +107,25 @@ typedef struct {
   const float* ln_c1;
   float ln_inv_k;
   float ln_eps;
+  /* GroupNorm(+activation) of the output applied by the split-K reduction in the same launch
+   * (ldm_conv2d_gn_fusable says whether a call takes it; ldm_conv2d refuses gn_out otherwise).
+   * Replaces: ldm_conv2d (split K, ResnetBlock2D conv1 / conv2 / Downsample2D at the 16x16 / 8x8 /
+   * mid levels, unet.py:361-425) + the ldm_group_norm of its output (ResnetBlock2D norm2 / the next
+   * block's norm1 / Transformer2DModel.norm).  One reduction block owns one image's 40-channel
+   * segment (whole groups), sums the K slabs in split order, applies the epilogue, rounds to bf16,
+   * takes exact fp64 per-unit (gn_unit channels) sums of the rounded values and forms each group's
+   * (mean, rstd) from them exactly as ldm_group_norm does from a producer's accumulators — so gn_out
+   * equals ldm_group_norm(out, those accumulators) bit for bit.  gn_partial, when set, receives the
+   * same unit sums (slot 0; the other slots stay zero).
+   * Scope: bf16, NHWC, no phase upsample, h_out * w_out in {32, 64, 128, 256}, n % 40 == 0,
+   * group size n / gn_groups in {4, 8, 20, 40}, gn_unit dividing the group size. */
+  void* gn_out;            /* NHWC bf16 [M][n] or NULL (off) */
+  const float* gn_gamma;   /* [n] */
+  const float* gn_beta;    /* [n] */
+  int gn_groups;
+  int gn_act;              /* LDM_ACT_NONE or LDM_ACT_SILU */
+  float gn_eps;
+  int gn_skip_out;         /* 1: `out` is not written (the pre-norm tensor is dead; out may alias gn_out) */
 } ldm_conv_params;
 
 /* Deep-K / few-tile shapes are split over K into an fp32 slab; this returns its size (0: none). */
@@ -117,6 +136,10 @@ int ldm_conv2d(const ldm_conv_params* p, ldm_stream_t stream);
  * 256x160 tile), out[1] bm, out[2] bn, out[3] ksplit, out[4] LDS stages.  LDM_OK or the
  * validation error ldm_conv2d would return. */
 int ldm_conv2d_describe_plan(const ldm_conv_params* p, int* out);
+/* 1 when ldm_conv2d(p) with gn_out / gn_gamma / gn_beta / gn_groups set applies the GroupNorm in the
+ * split-K reduction's launch (the plan splits K and the shape is in the fused kernel's scope), else 0
+ * (host only, no launch). */
+int ldm_conv2d_gn_fusable(const ldm_conv_params* p);
 /* Tuning hook (benchmarks and tests only, not thread-safe): force the tile plan of every
  * following ldm_conv2d call where it is legal — bm in {32, 64, 128} x bn in {32, 64, 128},
  * or bm = 256 for the large-tile bf16 kernel (bn 160); ksplit >= 1 (clamped).  bm = 0

@@ -638,6 +638,174 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(const ConvArgs p) 
   epilogue_rows<T, ROWS, COLS, 256>(p, m0, n0, raw, stage);
 }
 
+// Split-K reduction + epilogue + GroupNorm(+act) of the output in ONE launch (ldm_conv2d gn_out):
+// the deep levels' split convs (16x16 / 8x8 / mid; config 5's 8x16 / 4x8) are each followed by the
+// GroupNorm that normalises their output, and a group there is one image's 20-40 channels x 32-256
+// pixels — small enough for one block.  A block (10 channel quads x RPP row lanes) owns image b's
+// 40-channel segment n0..n0+39 (whole groups) and all of its hw = RPP * NP rows:
+//   1. issues every slab load of its rows (up to 16 float4 per thread in flight) together with the
+//      residual / time-embedding / bias loads, sums the ksplit fp32 slabs in split order (the same
+//      float adds as splitk_epilogue_kernel), applies bias, time embedding, activation and residual
+//      in epilogue_fast's order, rounds to bf16 and stores `out` (unless gn_skip_out);
+//   2. takes exact fp64 per-channel (sum, sumsq) of the rounded values, reduces them by a fixed
+//      two-level tree (8-row groups, then the groups in order) to gn_unit-channel units (written to
+//      gn_part slot 0 when asked) and to each group's (mean, rstd) exactly as gn_apply forms them
+//      from producer accumulators;
+//   3. writes gn_out = act(x * scale + shift) from the values still in registers.
+// Replaces splitk_epilogue_kernel + gn_apply (two launches and a re-read of the output).
+namespace sgn {
+constexpr int CS = 40, NQ = CS / 4;              // 40 channels = 10 quads per block
+}
+template <int RPP, int NP>
+__global__ __launch_bounds__(RPP * 10) void splitk_gn_kernel(const ConvArgs p) {
+  using namespace sgn;
+  constexpr int NT = RPP * NQ;
+  constexpr int G = 16 / NP;                     // splits whose loads are in flight together
+  constexpr int RG = RPP / 8;                    // 8-row groups of the statistics tree
+  __shared__ double red[NT * 8];                 // per thread: 4 channels x (sum, sumsq)
+  __shared__ double tre[RG * CS * 2];            // per (8-row group, channel)
+  __shared__ double chs[CS * 2];
+  __shared__ double uts[CS * 2];
+  __shared__ float2 gst[CS];
+  const int N = p.n, hw = p.hw_out;
+  const int segs = N / CS;
+  const int b = blockIdx.x / segs, n0 = (blockIdx.x - b * segs) * CS;
+  const int tid = threadIdx.x, q = tid % NQ, r0 = tid / NQ;
+  const int n = n0 + 4 * q;
+  const int64_t mb = (int64_t)b * hw;
+  const int64_t slab = (int64_t)p.M * N;
+  // epilogue operands first: their loads overlap the slab stream
+  float add[4], te[4] = {0.f, 0.f, 0.f, 0.f};
+  {
+    const float4 b4 = p.bias ? *reinterpret_cast<const float4*>(p.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
+    add[0] = b4.x; add[1] = b4.y; add[2] = b4.z; add[3] = b4.w;
+  }
+  if (p.temb) {
+    const float4 t4 = *reinterpret_cast<const float4*>(p.temb + (int64_t)b * p.temb_stride + n);
+    te[0] = t4.x; te[1] = t4.y; te[2] = t4.z; te[3] = t4.w;
+  }
+  const bf16_t* res = reinterpret_cast<const bf16_t*>(p.residual);
+  uint2 rv[NP];
+  if (res) {
+#pragma unroll
+    for (int j = 0; j < NP; ++j) rv[j] = *reinterpret_cast<const uint2*>(res + (mb + r0 + j * RPP) * N + n);
+  }
+  float v[NP][4];
+#pragma unroll
+  for (int j = 0; j < NP; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[j][k] = 0.f;
+  // the slabs are segment-major (ConvArgs::slab_seg): this block's rows of one split are one
+  // contiguous [hw][40] run, read lane-linearly (lane t of a pass at float 4t)
+  const float* src = p.partial + ((int64_t)b * segs * hw + (int64_t)(n0 / CS) * hw + r0) * CS + 4 * q;
+  for (int sp = 0; sp < p.ksplit; sp += G) {
+    float4 x[G][NP];
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+        if (sp + u < p.ksplit) x[u][j] = *reinterpret_cast<const float4*>(src + (sp + u) * slab + j * RPP * CS);
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+#pragma unroll
+      for (int j = 0; j < NP; ++j)
+        if (sp + u < p.ksplit) {
+          v[j][0] += x[u][j].x; v[j][1] += x[u][j].y; v[j][2] += x[u][j].z; v[j][3] += x[u][j].w;
+        }
+  }
+  // epilogue (epilogue_fast's order: + bias (0 without), + time embedding, act, + residual, bf16)
+  bf16_t* out = reinterpret_cast<bf16_t*>(p.out);
+  double s[4] = {0.0, 0.0, 0.0, 0.0}, sq[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    float rr[4] = {0.f, 0.f, 0.f, 0.f};
+    if (res) {
+      rr[0] = __uint_as_float(rv[j].x << 16); rr[1] = __uint_as_float(rv[j].x & 0xffff0000u);
+      rr[2] = __uint_as_float(rv[j].y << 16); rr[3] = __uint_as_float(rv[j].y & 0xffff0000u);
+    }
+    bf16_t h[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float y = v[j][k] + add[k];
+      if (p.temb) y += te[k];
+      if (p.act != LDM_ACT_NONE) y = act_f(y, p.act);
+      if (res) y += rr[k];
+      h[k] = f2bf(y);
+      v[j][k] = bf2f(h[k]);                         // the value as stored
+      s[k] += (double)v[j][k];
+      sq[k] += (double)v[j][k] * (double)v[j][k];   // exact: 8-bit mantissas
+    }
+    if (!p.gn_skip_out) *reinterpret_cast<uint2*>(out + (mb + r0 + j * RPP) * N + n) = *reinterpret_cast<const uint2*>(h);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { red[tid * 8 + 2 * k] = s[k]; red[tid * 8 + 2 * k + 1] = sq[k]; }
+  __syncthreads();
+  if (tid < RG * CS) {                              // (8-row group, channel): its rows in order
+    const int c = tid % CS, rg = tid / CS;
+    const int qc = c >> 2, k = c & 3;
+    double a = 0.0, e = 0.0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      a += red[((rg * 8 + r) * NQ + qc) * 8 + 2 * k];
+      e += red[((rg * 8 + r) * NQ + qc) * 8 + 2 * k + 1];
+    }
+    tre[(rg * CS + c) * 2] = a;
+    tre[(rg * CS + c) * 2 + 1] = e;
+  }
+  __syncthreads();
+  if (tid < CS) {                                   // channel: its row groups in order
+    double a = 0.0, e = 0.0;
+#pragma unroll
+    for (int rg = 0; rg < RG; ++rg) { a += tre[(rg * CS + tid) * 2]; e += tre[(rg * CS + tid) * 2 + 1]; }
+    chs[2 * tid] = a;
+    chs[2 * tid + 1] = e;
+  }
+  __syncthreads();
+  const int U = p.gn_unit, nu = CS / U;
+  if (tid < nu) {                                   // unit: its channels in order
+    double a = 0.0, e = 0.0;
+    for (int k = 0; k < U; ++k) { a += chs[2 * (tid * U + k)]; e += chs[2 * (tid * U + k) + 1]; }
+    uts[2 * tid] = a;
+    uts[2 * tid + 1] = e;
+    if (p.gn_part) {
+      double* d = p.gn_part + ((int64_t)b * p.gn_slots * (N / U) + n0 / U + tid) * 2;
+      d[0] = a;
+      d[1] = e;
+    }
+  }
+  __syncthreads();
+  const int cpg = N / p.gn_groups, upg = cpg / U;
+  if (tid < CS / cpg) {                             // group: its units in order (gn_apply's sums)
+    double sa = 0.0, sb = 0.0;
+    for (int k = 0; k < upg; ++k) { sa += uts[2 * (tid * upg + k)]; sb += uts[2 * (tid * upg + k) + 1]; }
+    const double cnt = (double)hw * cpg;
+    const double mean = sa / cnt;
+    double var = sb / cnt - mean * mean;
+    if (var < 0.0) var = 0.0;
+    gst[tid] = make_float2((float)mean, (float)(1.0 / sqrt(var + (double)p.gn_eps)));
+  }
+  __syncthreads();
+  float sc[4], sh[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float2 ms = gst[(4 * q + k) / cpg];
+    sc[k] = ms.y * p.gn_gamma[n + k];
+    sh[k] = fmaf(-ms.x, sc[k], p.gn_beta[n + k]);
+  }
+  bf16_t* go = reinterpret_cast<bf16_t*>(p.gn_out);
+#pragma unroll
+  for (int j = 0; j < NP; ++j) {
+    bf16_t h[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float y = fmaf(v[j][k], sc[k], sh[k]);
+      if (p.gn_act == LDM_ACT_SILU) y = silu_f(y);
+      h[k] = f2bf(y);
+    }
+    *reinterpret_cast<uint2*>(go + (mb + r0 + j * RPP) * N + n) = *reinterpret_cast<const uint2*>(h);
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Large-tile bf16 kernel for the big UNet GEMMs (64x64 / 32x32 levels, GEGLU, QKV).
 // Block tile 256 x 160 (160 divides every SD channel count: 320, 640, 960, 1280, 2560 ...),
@@ -1178,8 +1346,44 @@ void splitk_tile(int M, int n, int* rows, int* cols) {
     while (*rows > 16 && blocks(*rows, 64) < 512) *rows >>= 1;
 }
 
+// the fused split-K reduction + GroupNorm (splitk_gn_kernel) takes this call: its plan splits K and
+// the shape is in the kernel's scope (one block per image x 40-channel segment, hw = 32 * NP rows)
+bool gn_fusable_args(const ldm_conv_params* q, int ksplit) {
+  if (!q->gn_out || !q->gn_gamma || !q->gn_beta || ksplit <= 1) return false;
+  if (q->dtype != LDM_BF16 || q->out_layout != LDM_OUT_NHWC || q->out_f32 || q->upsample == 3) return false;
+  if (q->row_stats || q->ln_rows) return false;
+  const int hw = q->h_out * q->w_out;
+  if (hw != 32 && hw != 64 && hw != 128 && hw != 256) return false;
+  if (q->n % sgn::CS || q->gn_groups <= 0 || q->n % q->gn_groups) return false;
+  const int cpg = q->n / q->gn_groups;
+  const int unit = q->gn_unit > 0 ? q->gn_unit : 1;
+  if (cpg % 4 || sgn::CS % cpg || cpg % unit) return false;
+  if (q->gn_act != LDM_ACT_NONE && q->gn_act != LDM_ACT_SILU) return false;
+  // one block per (image, 40-channel segment): a single frame's 32 blocks (config 2) leave the chip
+  // idle and lose to the 512-block reduction + gn_apply pair (same-box A/B, B = 1: 4.149 -> 4.257 ms)
+  if (q->batch * (q->n / sgn::CS) < 128) return false;
+  const auto a8 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 7) == 0; };
+  const auto a16 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; };
+  if (!a8(q->out) || !a8(q->residual) || !a8(q->gn_out) || !a16(q->temb) || (q->temb && q->temb_stride % 4))
+    return false;
+  return true;
+}
+
+void launch_splitk_gn(const ConvArgs& a, hipStream_t s) {
+  const dim3 grid((a.M / a.hw_out) * (a.n / sgn::CS));
+  // 64 row lanes (640 threads) from 64 rows up: every slab load of a thread in flight at once
+  if (a.hw_out == 32) hipLaunchKernelGGL((splitk_gn_kernel<32, 1>), grid, dim3(320), 0, s, a);
+  else if (a.hw_out == 64) hipLaunchKernelGGL((splitk_gn_kernel<64, 1>), grid, dim3(640), 0, s, a);
+  else if (a.hw_out == 128) hipLaunchKernelGGL((splitk_gn_kernel<64, 2>), grid, dim3(640), 0, s, a);
+  else hipLaunchKernelGGL((splitk_gn_kernel<64, 4>), grid, dim3(640), 0, s, a);
+}
+
 template <typename T>
 void launch_splitk_epilogue(const ConvArgs& a, hipStream_t s) {
+  if (a.gn_out) {                      // the GroupNorm of the output in the same launch
+    launch_splitk_gn(a, s);
+    return;
+  }
   int rows, cols;
   splitk_tile(a.M, a.n, &rows, &cols);
   const dim3 grid(((a.M + rows - 1) / rows) * ((a.n + cols - 1) / cols));
@@ -1626,6 +1830,24 @@ extern "C" int ldm_conv2d_describe_plan(const ldm_conv_params* q, int* out) {
   return LDM_OK;
 }
 
+// the split-K factor ldm_conv2d runs for q (validated)
+int plan_ksplit(const ldm_conv_params* q, int es) {
+  const int M = q->batch * q->h_out * q->w_out;
+  const bool mixed = is_mixed(q, es);
+  const int hks = halo_plan(q, es, mixed);
+  if (hks) return hks;
+  ldm_igemm::RingCfg rc{0, 0, 0, 1};
+  if (ldm_igemm::ring_cfg(q, es, mixed, M, g_force_bm != 0, &rc)) return std::max(1, rc.ks);
+  if (ldm_igemm::wide_bm(q, es, mixed, M, g_force_bm != 0) || use_ars(q, es, mixed, M)) return 1;
+  return make_plan(q, M, es, mixed).ksplit;
+}
+
+extern "C" int ldm_conv2d_gn_fusable(const ldm_conv_params* q) {
+  int es = 0;
+  if (validate(q, &es) != LDM_OK) return 0;
+  return gn_fusable_args(q, plan_ksplit(q, es)) ? 1 : 0;
+}
+
 extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   int es = 0;
   const int st = validate(q, &es);
@@ -1647,6 +1869,7 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
     const size_t need = (size_t)pl.ksplit * M * q->n * sizeof(float);
     if (!q->workspace || q->workspace_bytes < (int64_t)need || !aligned16(q->workspace)) return LDM_ERR_ARG;
   }
+  if (q->gn_out && !gn_fusable_args(q, pl.ksplit)) return LDM_ERR_ARG;   // ask ldm_conv2d_gn_fusable first
 
   ConvArgs a{};
   a.a0 = static_cast<const char*>(q->a0);
@@ -1683,6 +1906,14 @@ extern "C" int ldm_conv2d(const ldm_conv_params* q, ldm_stream_t stream) {
   a.ln_c1 = q->ln_c1;
   a.ln_inv_k = q->ln_inv_k;
   a.ln_eps = q->ln_eps;
+  a.gn_out = static_cast<char*>(q->gn_out);
+  a.gn_gamma = q->gn_gamma;
+  a.gn_beta = q->gn_beta;
+  a.gn_groups = q->gn_groups;
+  a.gn_act = q->gn_act;
+  a.gn_eps = q->gn_eps;
+  a.gn_skip_out = q->gn_skip_out ? 1 : 0;
+  a.slab_seg = q->gn_out ? 1 : 0;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (use_halo) return launch_halo(a, s);
   if (ring) {

@@ -39,6 +39,14 @@ struct ConvArgs {
   int phase;          // nearest-2x upsample + 3x3 conv as four 2x2 phase convs (ldm_conv2d upsample 3):
                       // rows m = (b, phase, y, x) over the low-res grid, W = [4][n][kpad]
   int abl;            // ablation mode of the deep-ring GEMM (tuning hook; 0 = normal)
+  // GroupNorm(+act) of the output fused into the split-K reduction (splitk_gn_kernel); gn_out NULL = off
+  char* gn_out;
+  const float* gn_gamma;
+  const float* gn_beta;
+  int gn_groups, gn_act, gn_skip_out;
+  float gn_eps;
+  int slab_seg;       // 1 (with gn_out): split-K slabs laid out [ks][batch][n / 40][hw][40] so the fused
+                      // reduction's block (one image x 40 channels) reads one contiguous run per split
 };
 // deep-ring 1x1 GEMM configuration (gemm_ring.hip): id 0 = not the ring kernel
 struct RingCfg { int id, bm, bn, ks; };   // ks: K splits (fp32 slabs + the split-K reduction kernel)
@@ -759,6 +767,23 @@ __device__ __forceinline__ void write_partial_rows(const ConvArgs& p, float* par
                                                    const float* stage, int pitch) {
   constexpr int CW = COLS / 4, RP = NT / CW, NP = (ROWS + RP - 1) / RP;
   const int tid = threadIdx.x, c4 = tid % CW, r0 = tid / CW;
+  if constexpr (COLS % 40 == 0) {
+    // segment-major slab (ConvArgs::slab_seg, the fused split-K GroupNorm): a full tile inside one
+    // image is COLS / 40 contiguous runs of ROWS x 40 floats; lanes walk each run linearly
+    const int b = m0 / p.hw_out, pix0 = m0 - b * p.hw_out;
+    if (p.slab_seg && pix0 + ROWS <= p.hw_out && m0 + ROWS <= p.M && n0 % 40 == 0) {
+      constexpr int RUN = ROWS * 10, TOT = (COLS / 40) * RUN;      // float4 per run / per tile
+      float* base = part + (((int64_t)b * (p.n / 40) + n0 / 40) * p.hw_out + pix0) * 40;
+#pragma unroll 4
+      for (int l = tid; l < TOT; l += NT) {
+        const int sg = l / RUN, w = l - sg * RUN, r = w / 10, qd = w - r * 10;
+        if (n0 + sg * 40 >= p.n) break;
+        *reinterpret_cast<float4*>(base + (int64_t)sg * p.hw_out * 40 + 4 * w) =
+            *reinterpret_cast<const float4*>(stage + r * pitch + sg * 40 + 4 * qd);
+      }
+      return;
+    }
+  }
   const int n = n0 + 4 * c4;
   if (r0 >= RP || n >= p.n) return;
 #pragma unroll
@@ -766,6 +791,11 @@ __device__ __forceinline__ void write_partial_rows(const ConvArgs& p, float* par
     const int r = r0 + q * RP, m = m0 + r;
     if (r >= ROWS || m >= p.M) break;
     const float4 x = *reinterpret_cast<const float4*>(stage + r * pitch + 4 * c4);
+    if (p.slab_seg) {               // [batch][n / 40][hw][40] (n % 40 == 0: a float4 stays in its segment)
+      const int b = m / p.hw_out, pix = m - b * p.hw_out, sg = n / 40;
+      *reinterpret_cast<float4*>(part + (((int64_t)b * (p.n / 40) + sg) * p.hw_out + pix) * 40 + (n - sg * 40)) = x;
+      continue;
+    }
     float* dst = part + (int64_t)m * p.n + n;
     if (n + 3 < p.n) {
       *reinterpret_cast<float4*>(dst) = x;

@@ -509,7 +509,19 @@ class UNet(nn.Module):
         self._plan = self._plan_key = self._dplan = None
 
     # ------------------------------------------------------------ HIP forward pieces
-    def _resnet(self, P, r, xs, B, H, W, temb_all):
+    def _gn_next(self, P, m):
+        """conv2d(gn_next=...) spec of the GroupNorm that consumes a block output next: a ResnetBlock2D's
+        norm1 (+SiLU) or a Transformer2DModel's norm (no activation); None when the consumer reads a
+        concat or no GroupNorm (the split-K reduction then only emits the statistics)."""
+        if m is None:
+            return None
+        if isinstance(m, ResnetBlock2D):
+            return (m.groups, *P[id(m)]["n1"], m.eps, K.ACT_SILU, True)
+        return (m.groups, *P[id(m)]["norm"], 1e-6, K.ACT_NONE, True)
+
+    def _resnet(self, P, r, xs, B, H, W, temb_all, gn_next=None):
+        """gn_next: the GroupNorm consuming this block's output (see _gn_next); the deep levels' split
+        convs apply it (and norm2 after conv1) in their split-K reduction's launch."""
         p = P[id(r)]
         x0, x1 = xs
         side = None
@@ -523,7 +535,8 @@ class UNet(nn.Module):
             with torch.cuda.stream(side):
                 res = K.conv2d(p["sc"], x0, B, H, W, x1=x1)
         h = K.group_norm(x0, B, H * W, r.groups, *p["n1"], r.eps, K.ACT_SILU, x1=x1)
-        h = K.conv2d(p["c1"], h, B, H, W, temb=temb_all[:, p["off"]:], temb_stride=temb_all.shape[1], gn_stats=True)
+        h = K.conv2d(p["c1"], h, B, H, W, temb=temb_all[:, p["off"]:], temb_stride=temb_all.shape[1], gn_stats=True,
+                     gn_next=(r.groups, *p["n2"], r.eps, K.ACT_SILU, False))
         h = K.group_norm(h, B, H * W, r.groups, *p["n2"], r.eps, K.ACT_SILU)
         if side is not None:
             main.wait_stream(side)
@@ -533,7 +546,7 @@ class UNet(nn.Module):
         else:
             assert x1 is None
             res = x0
-        return K.conv2d(p["c2"], h, B, H, W, residual=res, gn_stats=True)
+        return K.conv2d(p["c2"], h, B, H, W, residual=res, gn_stats=True, gn_next=gn_next)
 
     def _side_stream(self, dev):
         st = getattr(self, "_side", None)
@@ -764,25 +777,40 @@ class UNet(nn.Module):
             main.wait_stream(side)
             temb_all.record_stream(main)
         skips = [(x, H, W)]
-        for blk in self.down_blocks:
+        mb = self.mid_block
+        nb = len(self.down_blocks)
+        for bi, blk in enumerate(self.down_blocks):
             for j, r in enumerate(blk.resnets):
-                x = self._resnet(P, r, (x, None), B, H, W, temb_all)
+                # the GroupNorm that reads this resnet's output next (applied in its conv2's split-K
+                # reduction where the plan splits: the 16x16 / 8x8 levels)
+                if blk.has_cross_attention:
+                    nxt = blk.attentions[j]
+                elif j + 1 < len(blk.resnets):
+                    nxt = blk.resnets[j + 1]
+                elif blk.downsamplers is None:
+                    nxt = mb.resnets[0] if bi + 1 == nb else self.down_blocks[bi + 1].resnets[0]
+                else:
+                    nxt = None
+                x = self._resnet(P, r, (x, None), B, H, W, temb_all, gn_next=self._gn_next(P, nxt))
                 if blk.has_cross_attention:
                     x = self._transformer(P, blk.attentions[j], x, B, H, W, encoder_hidden_states)
                 skips.append((x, H, W))
             if blk.downsamplers is not None:
-                x = K.conv2d(P[id(blk.downsamplers[0])], x, B, H, W, stride=2, gn_stats=True)
+                nxt = self.down_blocks[bi + 1].resnets[0] if bi + 1 < nb else mb.resnets[0]
+                x = K.conv2d(P[id(blk.downsamplers[0])], x, B, H, W, stride=2, gn_stats=True,
+                             gn_next=self._gn_next(P, nxt))
                 H, W = (H + 1) // 2, (W + 1) // 2
                 skips.append((x, H, W))
-        mb = self.mid_block
-        x = self._resnet(P, mb.resnets[0], (x, None), B, H, W, temb_all)
+        x = self._resnet(P, mb.resnets[0], (x, None), B, H, W, temb_all, gn_next=self._gn_next(P, mb.attentions[0]))
         x = self._transformer(P, mb.attentions[0], x, B, H, W, encoder_hidden_states)
         x = self._resnet(P, mb.resnets[1], (x, None), B, H, W, temb_all)
         for blk in self.up_blocks:
             for j, r in enumerate(blk.resnets):
                 s, sh, sw = skips.pop()
                 assert (sh, sw) == (H, W)
-                x = self._resnet(P, r, (x, s), B, H, W, temb_all)      # cat([x, skip]) read in place
+                # (the next resnet's norm1 reads [x || skip]: only a transformer's norm is applied early)
+                nxt = blk.attentions[j] if blk.has_cross_attention else None
+                x = self._resnet(P, r, (x, s), B, H, W, temb_all, gn_next=self._gn_next(P, nxt))  # cat read in place
                 if blk.has_cross_attention:
                     x = self._transformer(P, blk.attentions[j], x, B, H, W, encoder_hidden_states)
             if blk.upsamplers is not None:

@@ -35,7 +35,9 @@ class ConvParams(ctypes.Structure):
                 ("n", _i), ("kpad", _i), ("bias", _vp), ("temb", _vp), ("temb_stride", _i), ("residual", _vp),
                 ("out", _vp), ("out_layout", _i), ("act", _i), ("dtype", _i), ("out_f32", _i),
                 ("workspace", _vp), ("workspace_bytes", _i64), ("gn_partial", _vp), ("pad_mode", _i), ("gn_unit", _i), ("gn_slots", _i),
-                ("row_stats", _vp), ("ln_rows", _vp), ("ln_c1", _vp), ("ln_inv_k", _f), ("ln_eps", _f)]
+                ("row_stats", _vp), ("ln_rows", _vp), ("ln_c1", _vp), ("ln_inv_k", _f), ("ln_eps", _f),
+                ("gn_out", _vp), ("gn_gamma", _vp), ("gn_beta", _vp), ("gn_groups", _i), ("gn_act", _i),
+                ("gn_eps", _f), ("gn_skip_out", _i)]
 
 
 class GnFold(ctypes.Structure):
@@ -78,6 +80,7 @@ EXPORTS = {
     "ldm_conv2d_workspace_bytes": (ctypes.c_size_t, [ctypes.POINTER(ConvParams)]),
     "ldm_conv2d_force_plan": (None, [_i, _i, _i]),
     "ldm_conv2d_describe_plan": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ctypes.c_int)]),
+    "ldm_conv2d_gn_fusable": (_i, [ctypes.POINTER(ConvParams)]),
     "ldm_conv2d_force_stages": (None, [_i]),
     "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_conv2d_set_halo": (None, [_i]),
@@ -396,6 +399,12 @@ def packed_rows(t, bias=None):
 
 
 GN_PART_ATTR = "_ldm_gn_part"
+GN_DONE_ATTR = "_ldm_gn_done"     # (key, normalised tensor) a split-K conv's reduction already produced
+
+
+def gn_key(groups, gamma, beta, eps, act):
+    """Identity of one GroupNorm application (ldm_conv2d gn_out <-> group_norm)."""
+    return (int(groups), gamma.data_ptr(), beta.data_ptr(), float(eps), int(act))
 
 
 def gn_stats_of(t):
@@ -463,14 +472,30 @@ def _gn_accumulators(batch, slots, n, device):
     return torch.zeros(batch, slots, n, 2, dtype=torch.float64, device=device)
 
 
+GN_FUSE = True            # A/B hook (set_gn_fuse): GroupNorm in the split-K reduction's launch
+
+
+def set_gn_fuse(enabled=True):
+    """A/B hook: let conv2d(gn_next=...) run the consumer GroupNorm inside the split-K reduction
+    (default on); off runs the reduction and ldm_group_norm as two launches."""
+    global GN_FUSE
+    GN_FUSE = bool(enabled)
+
+
 def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False, temb=None, temb_stride=0,
            residual=None, out=None, out_layout=OUT_NHWC, act=ACT_NONE, out_dtype=None, gn_stats=False, pad_mode=0,
-           row_stats=None, ln=None):
+           row_stats=None, ln=None, gn_next=None):
     """Run ldm_conv2d.  x0/x1: NHWC [batch, h, w, c] (any contiguous view with that numel).
 
     gn_stats=True also has the epilogue sum the per-(batch, channel) (sum, sumsq) of the output
     into fp64 accumulators (from the enclosing gn_arena when there is one); they are attached to
     the returned tensor and consumed by group_norm().
+
+    gn_next = (groups, gamma, beta, eps, act, keep_out): the GroupNorm that will consume the output.
+    When the plan splits K and the shape is in scope (ldm_conv2d_gn_fusable: the deep levels), the
+    reduction applies it in the same launch and the normalised tensor is attached to the output, so
+    the following group_norm() with the same arguments returns it without a launch.  keep_out=False:
+    the pre-norm output is dead — it is not written and the normalised tensor is returned instead.
 
     row_stats: a zeroed fp64 [M, 2] tensor the epilogue adds each output row's (sum, sumsq) to.
     ln = (rows, eps): x0's rows are LayerNorm'd inside the GEMM (pc from packed_ln_fold, rows =
@@ -551,9 +576,31 @@ def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False
     if ws_bytes:
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=x0.device)
         p.workspace, p.workspace_bytes = _ptr(ws), ws_bytes
+    gn_done = None
+    if gn_next is not None and ws_bytes and GN_FUSE and odt == torch.bfloat16 and out_layout == OUT_NHWC:
+        groups, gamma, beta, eps, gact, keep = gn_next
+        _gpu(gamma, beta)
+        if gamma.dtype != torch.float32 or beta.dtype != torch.float32 or gamma.numel() != n or beta.numel() != n:
+            raise ValueError("gn_next gamma / beta must be fp32 [n]")
+        p.gn_out, p.gn_gamma, p.gn_beta = p.out, _ptr(gamma), _ptr(beta)
+        p.gn_groups, p.gn_act, p.gn_eps = int(groups), int(gact), float(eps)
+        if not p.gn_unit:
+            p.gn_unit = gn_unit_for(n)
+        if lib.ldm_conv2d_gn_fusable(ctypes.byref(p)):
+            if keep:
+                gout = torch.empty_like(out)
+                p.gn_out = _ptr(gout)
+            else:                          # the pre-norm tensor is dead: normalise into out itself
+                gout, part = out, None
+                p.gn_skip_out, p.gn_partial = 1, None
+            gn_done = (gn_key(groups, gamma, beta, eps, gact), gout)
+        else:
+            p.gn_out = p.gn_gamma = p.gn_beta = None
+            p.gn_groups = p.gn_act = 0
     ev = _prof_start()
     _check(lib.ldm_conv2d(ctypes.byref(p), _stream(x0)), "ldm_conv2d")
     setattr(out, GN_PART_ATTR, part)     # never leave a stale slab on a rewritten tensor
+    setattr(out, GN_DONE_ATTR, gn_done)
     if ev is not None:
         flops = 2.0 * M * n * pc.ksize * pc.ksize * pc.cin_real
         nbytes = (x0.numel() + (0 if x1 is None else x1.numel()) + pc.w.numel()) * x0.element_size() + \
@@ -1011,6 +1058,9 @@ def group_norm(x0, batch, hw, groups, gamma, beta, eps, act=ACT_NONE, x1=None, o
 
     The one-launch kernel stages <= 64 groups and <= 2560 channels in LDS (every SD-1.x UNet,
     seg-VAE and PoseExpNet width fits); wider calls are refused here, before any launch."""
+    done = getattr(x0, GN_DONE_ATTR, None)
+    if done is not None and x1 is None and out is None and done[0] == gn_key(groups, gamma, beta, eps, act):
+        return done[1]                    # applied by the producing conv's split-K reduction
     c_all = (x0.numel() + (0 if x1 is None else x1.numel())) // max(1, batch * hw)
     if groups > GN_MAX_GROUPS or c_all > GN_MAX_CHANNELS or groups <= 0 or c_all % groups:
         raise ValueError(f"group_norm: {groups} groups over {c_all} channels is outside the HIP kernel's range "
