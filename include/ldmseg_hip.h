@@ -140,6 +140,9 @@ int ldm_conv2d_describe_plan(const ldm_conv_params* p, int* out);
  * split-K reduction's launch (the plan splits K and the shape is in the fused kernel's scope), else 0
  * (host only, no launch). */
 int ldm_conv2d_gn_fusable(const ldm_conv_params* p);
+/* Tuning hook: the fewest reduction blocks (images x 40-channel segments) the fused GroupNorm takes
+ * (default 16: every in-scope call; smaller grids keep the two launches). */
+void ldm_conv2d_set_gn_fuse_min_blocks(int n);
 /* Tuning hook (benchmarks and tests only, not thread-safe): force the tile plan of every
  * following ldm_conv2d call where it is legal — bm in {32, 64, 128} x bn in {32, 64, 128},
  * or bm = 256 for the large-tile bf16 kernel (bn 160); ksplit >= 1 (clamped).  bm = 0

@@ -12,8 +12,8 @@ Bars:
   - against the two-launch path (whose statistics are fp32 tile partials) within 1e-2 of the
     tensor scale, and against torch fp32 F.group_norm (+ F.silu) of the same output within 1e-2;
   - gn_skip_out (the pre-norm tensor dead) gives the same normalised bits.
-Shapes: every deep-level shape of the headline B = 8 step, the smallest grid the planner fuses
-(B = 4) and config 5 (B = 16, 8x16 / 4x8; config 2's single frame keeps the two launches), incl. time embedding, residual, stride-2 Downsample2D, 20-channel groups.
+Shapes: every deep-level shape of the headline B = 8 step, of config 2 (B = 1: 16-32 blocks) and
+of config 5 (B = 16, 8x16 / 4x8), incl. time embedding, residual, stride-2 Downsample2D, 20-channel groups.
 """
 import pytest
 import torch
@@ -57,8 +57,9 @@ SHAPES = [
     (8, 16, 16, 1280, 1280, 3, 1, False, True, K.ACT_NONE),     # 16x16 conv2 -> transformer norm
     (8, 32, 32, 640, 640, 3, 2, False, False, K.ACT_SILU),      # Downsample2D 32 -> 16, 20-ch groups
     (8, 16, 16, 1280, 1280, 3, 2, False, False, K.ACT_SILU),    # Downsample2D 16 -> 8
-    (4, 8, 8, 1280, 1280, 3, 1, True, False, K.ACT_SILU),       # the smallest grid taken (128 blocks)
-    (4, 16, 16, 1280, 1280, 3, 1, False, True, K.ACT_NONE),
+    (1, 8, 8, 1280, 1280, 3, 1, True, False, K.ACT_SILU),       # config 2 (B = 1): 32 blocks
+    (1, 16, 16, 1280, 1280, 3, 1, False, True, K.ACT_NONE),
+    (1, 32, 32, 640, 640, 3, 2, False, False, K.ACT_SILU),      # 16 blocks
     (16, 8, 16, 1280, 1280, 3, 1, True, False, K.ACT_SILU),     # config 5 (T = 16, 32x64 latents)
     (16, 4, 8, 1280, 1280, 3, 1, False, True, K.ACT_SILU),
 ]
@@ -104,7 +105,7 @@ def test_splitk_gn_fused(B, H, W, cin, cout, k, stride, temb, res, gact):
 
 
 def test_splitk_gn_out_of_scope_falls_back():
-    """An unsplit plan (the 64x64 level) or a single frame's grid does not take gn_out: the conv stores its statistics and the
+    """An unsplit plan (the 64x64 level) or a grid below the hook's minimum does not take gn_out: the conv stores its statistics and the
     GroupNorm runs as its own launch; a different GroupNorm than the one announced never reuses the
     fused result."""
     B, H, W, C, G = 2, 64, 64, 320, 32
@@ -115,9 +116,13 @@ def test_splitk_gn_out_of_scope_falls_back():
     with torch.no_grad():
         t = F.silu(F.group_norm(out.float().permute(0, 3, 1, 2), G, gamma, beta, 1e-5))
     assert rel_err(y.reshape(B, H, W, C).permute(0, 3, 1, 2), t) < 1e-2
-    # a single frame (config 2): 32 reduction blocks would leave the chip idle -> two launches
+    # grids below the min-blocks hook keep the two launches
     pc, x, kw, _, gamma, beta = _case(1, 8, 8, 1280, 1280, 3, 1, True, False, K.ACT_SILU, seed=9)
-    out = K.conv2d(pc, x, 1, 8, 8, gn_next=(32, gamma, beta, 1e-5, K.ACT_SILU, True), **kw)
+    K.set_gn_fuse_min_blocks(64)
+    try:
+        out = K.conv2d(pc, x, 1, 8, 8, gn_next=(32, gamma, beta, 1e-5, K.ACT_SILU, True), **kw)
+    finally:
+        K.set_gn_fuse_min_blocks(16)
     assert getattr(out, K.GN_DONE_ATTR) is None
     pc, x, kw, _, gamma, beta = _case(8, 8, 8, 1280, 1280, 3, 1, True, False, K.ACT_SILU, seed=8)
     out = K.conv2d(pc, x, 8, 8, 8, gn_next=(32, gamma, beta, 1e-5, K.ACT_SILU, True), **kw)
@@ -129,7 +134,7 @@ def test_splitk_gn_out_of_scope_falls_back():
     assert rel_err(other.reshape(8, 8, 8, 1280).permute(0, 3, 1, 2), t) < 1e-2
 
 
-@pytest.mark.parametrize("B", [8])
+@pytest.mark.parametrize("B", [1, 8])
 def test_unet_sd14_gn_fuse_vs_unfused(B):
     """The SD-1.4 UNet (random init, bf16, 64x64 latents) with the deep levels' GroupNorms in the
     split-K reductions vs the two-launch path: the same model output within the bf16 bar, and the

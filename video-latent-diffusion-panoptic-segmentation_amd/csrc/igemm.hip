@@ -1346,6 +1346,8 @@ void splitk_tile(int M, int n, int* rows, int* cols) {
     while (*rows > 16 && blocks(*rows, 64) < 512) *rows >>= 1;
 }
 
+int g_gn_fuse_min_blocks = 16;    // tuning hook (ldm_conv2d_set_gn_fuse_min_blocks)
+
 // the fused split-K reduction + GroupNorm (splitk_gn_kernel) takes this call: its plan splits K and
 // the shape is in the kernel's scope (one block per image x 40-channel segment, hw = 32 * NP rows)
 bool gn_fusable_args(const ldm_conv_params* q, int ksplit) {
@@ -1359,9 +1361,10 @@ bool gn_fusable_args(const ldm_conv_params* q, int ksplit) {
   const int unit = q->gn_unit > 0 ? q->gn_unit : 1;
   if (cpg % 4 || sgn::CS % cpg || cpg % unit) return false;
   if (q->gn_act != LDM_ACT_NONE && q->gn_act != LDM_ACT_SILU) return false;
-  // one block per (image, 40-channel segment): a single frame's 32 blocks (config 2) leave the chip
-  // idle and lose to the 512-block reduction + gn_apply pair (same-box A/B, B = 1: 4.149 -> 4.257 ms)
-  if (q->batch * (q->n / sgn::CS) < 128) return false;
+  // one block per (image, 40-channel segment): even a single frame's 16-32 blocks (config 2) gain over
+  // the 512-block reduction + gn_apply pair (same-box A/B, B = 1: 4.310 -> 4.273 ms; the first form,
+  // row-major slabs and 320 threads, had lost: 4.149 -> 4.257)
+  if (q->batch * (q->n / sgn::CS) < g_gn_fuse_min_blocks) return false;
   const auto a8 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 7) == 0; };
   const auto a16 = [](const void* x) { return (reinterpret_cast<uintptr_t>(x) & 15) == 0; };
   if (!a8(q->out) || !a8(q->residual) || !a8(q->gn_out) || !a16(q->temb) || (q->temb && q->temb_stride % 4))
@@ -1777,6 +1780,7 @@ extern "C" void ldm_conv2d_set_splitk_cols(int cols) { g_splitk_cols = (cols == 
 extern "C" void ldm_conv2d_set_splitk_rows(int rows) {
   g_splitk_rows = (rows == 16 || rows == 32 || rows == 64) ? rows : 0;
 }
+extern "C" void ldm_conv2d_set_gn_fuse_min_blocks(int n) { g_gn_fuse_min_blocks = n > 0 ? n : 16; }
 extern "C" void ldm_conv2d_set_epilogue(int mode) { g_epi_pre = mode == 1 ? 0 : 1; }
 extern "C" void ldm_conv2d_force_stages(int stages) {
   g_force_stages = (stages == 1 || stages == 3 || stages == 4) ? stages : 0;   // 1: register-staged operands

@@ -81,6 +81,7 @@ EXPORTS = {
     "ldm_conv2d_force_plan": (None, [_i, _i, _i]),
     "ldm_conv2d_describe_plan": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ctypes.c_int)]),
     "ldm_conv2d_gn_fusable": (_i, [ctypes.POINTER(ConvParams)]),
+    "ldm_conv2d_set_gn_fuse_min_blocks": (None, [_i]),
     "ldm_conv2d_force_stages": (None, [_i]),
     "ldm_conv2d_set_raster_group": (None, [_i]),
     "ldm_conv2d_set_halo": (None, [_i]),
@@ -480,6 +481,12 @@ def set_gn_fuse(enabled=True):
     (default on); off runs the reduction and ldm_group_norm as two launches."""
     global GN_FUSE
     GN_FUSE = bool(enabled)
+
+
+def set_gn_fuse_min_blocks(n=16):
+    """Tuning hook: the fewest reduction blocks (images x 40-channel segments) the fused split-K
+    GroupNorm takes (ldm_conv2d_set_gn_fuse_min_blocks; smaller grids keep the two launches)."""
+    load_library().ldm_conv2d_set_gn_fuse_min_blocks(int(n))
 
 
 def conv2d(pc: PackedConv, x0, batch, h, w, *, x1=None, stride=1, upsample=False, temb=None, temb_stride=0,
