@@ -315,12 +315,15 @@ def test_attention_d80_forms_agree(B, N):
     assert torch.allclose(outs[0][1], outs[1][1], atol=2e-2)
 
 
-@pytest.mark.parametrize("B,N", [(4, 4096), (4, 4096 + 37), (4, 64 * 3 + 5)])
+@pytest.mark.parametrize("B,N", [(4, 4096), (4, 4096 + 37), (4, 64 * 3 + 5), (8, 4096 + 37)])
 def test_attention_d40_qs2_close_to_default(B, N):
     """head_dim 40 under the alternative kernels of ldm_attention_set_qs2 against the default and a
     torch fp32 reference on the device: mode 1 (two 32-query subtiles per wave; the shared rescale
     decision moves m by different bf16 steps, so within bf16 rounding, not bit-identical) and mode 2
-    (the software-pipelined tile loop: the same operations per query, bit-identical).  Ragged N
+    (the software-pipelined tile loop: the same operations per query, bit-identical), and the default
+    two-subtile interleaved kernel (ldm_attention_set_il, each subtile with its own rescale decision:
+    the 32-query kernel's arithmetic, bit-identical; taken from 256 blocks, B = 4 / 8 at N = 4096)
+    against the 32-query kernel it replaces.  Ragged N
     exercises the masked last key tile and the partial query block; N = 197 gives 4 key tiles (the
     pipeline's two-tile unroll with an odd tail)."""
     torch.manual_seed(9)
@@ -331,17 +334,23 @@ def test_attention_d40_qs2_close_to_default(B, N):
                      for b in range(B)]).permute(0, 2, 1, 3).reshape(B, N, C)
     outs = []
     try:
-        K.set_attention_kvsplit(0)          # mode 0 = the unsplit default kernel
+        K.set_attention_kvsplit(0)          # unsplit kernels only
+        K.set_attention_il(False)           # mode 0 = the 32-query kernel
         for mode in (0, 1, 2):
             K.set_attention_qs2(mode)
             outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, 40, N, N, 3 * C, 3 * C, 3 * C).float())
+        K.set_attention_qs2(0)
+        K.set_attention_il(True)
+        outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, 40, N, N, 3 * C, 3 * C, 3 * C).float())
     finally:
         K.set_attention_qs2(0)
+        K.set_attention_il(True)
         K.set_attention_kvsplit(-1)
     for o in outs:
         assert ((o - ref).norm() / ref.norm()).item() < 1e-2
     assert (outs[0] - outs[1]).abs().max().item() < 0.05
     assert torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0], outs[3])
 
 
 @pytest.mark.parametrize("B,N,hd", [(4, 4096, 40), (4, 4096 + 37, 40), (4, 64 * 3 + 5, 40), (4, 64, 40), (4, 40, 40),

@@ -51,12 +51,13 @@ def mm_case(M, K, N):
 
 
 def attn_case(B, N, C, heads=8, legacy=False, waves=0, maxcol=2, fp8=False, scaled=True, d80=True, qs2=0, skew=0,
-              pair=True):
+              pair=True, il=True):
     qkv = torch.randn(B, N, 3 * C, device=DEV).to(BF)
 
     def run():
         K.set_attention_d80(d80)
         K.set_attention_qs2(qs2)
+        K.set_attention_il(il)
         K.set_attention_skew(skew)
         K.set_attention_pair(pair)
         K.force_attention_legacy(legacy)
@@ -381,6 +382,8 @@ CASES = {
     "attn_c5_2048_d40_noskew": lambda: attn_case(16, 2048, 320, skew=1),
     "attn_c5_2048_d40_skew": lambda: attn_case(16, 2048, 320, skew=2),
     "attn_4096_d40_pipe": lambda: attn_case(8, 4096, 320, qs2=2),
+    "attn_4096_d40_noil": lambda: attn_case(8, 4096, 320, il=False),
+    "attn_c5_2048_d40_noil": lambda: attn_case(16, 2048, 320, il=False),
     "attn_c5_2048_d40_qs2": lambda: attn_case(16, 2048, 320, qs2=1),
     "attn_c5_2048_d40_pipe": lambda: attn_case(16, 2048, 320, qs2=2),
     "attn_c5_2048_d40_fp8_qs2": lambda: attn_case(16, 2048, 320, fp8=True, qs2=1),

@@ -728,8 +728,13 @@ template <int V>
 struct IntC {
   static constexpr int value = V;
 };
+// IL (QS = 2): the two query subtiles' phases interleaved inside each wave — S(1) = K Q1^T beside the
+// exp / cvt of subtile 0, O(0) += V^T P0^T beside those of subtile 1 — so the wave's own VALU work
+// fills the issue slots its MFMAs leave (the same-wave interleave overlaps where two waves on a SIMD
+// do not: tools/mfma_valu_overlap.hip).  Each subtile keeps its own running-max decision, i.e. the
+// QS = 1 kernel's per-wave arithmetic: bit-identical to it.
 template <int NW, int OCC, int KT = 64, int D = 40, int QS = 1, bool SKEW = false, bool KVS = false,
-          bool PAIR = false>
+          bool PAIR = false, bool IL = false>
 __global__ __launch_bounds__(64 * NW, PAIR ? (OCC * NW + 3) / 4 : OCC) void attn_d40_kernel(const AttnArgs p) {
   typedef bf16_t T;
   typedef __attribute__((ext_vector_type(16))) float f32x16_t;
@@ -960,7 +965,96 @@ __global__ __launch_bounds__(64 * NW, PAIR ? (OCC * NW + 3) / 4 : OCC) void attn
         }
     }
   };
+  static_assert(!IL || (QS == 2 && !SKEW && !KVS && !PAIR), "IL interleaves the two subtiles of the plain loop");
+  auto compute_il = [&](int buf, int kv0, bool masked, bool first, int half) {
+    const T* Ks = lds + buf * 2 * TILE + half * 64 * ROW;
+    const T* Vs = lds + buf * 2 * TILE + TILE + half * 64 * ROW;
+    kv0 += 64 * half;
+    f32x16_t sacc[2][2];
+    uint4 ka[2][QC];                                 // K fragments, shared by both subtiles
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int c = 0; c < QC; ++c) ka[blk][c] = *reinterpret_cast<const uint4*>(Ks + (32 * blk + r32) * ROW + 8 * hh + 16 * c);
+    auto qk1 = [&](int s) __attribute__((always_inline)) {
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[s][blk][r] = 0.f;
+#pragma unroll
+        for (int c = 0; c < QC; ++c)
+          sacc[s][blk] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, ka[blk][c]),
+                                                                 __builtin_bit_cast(bf16x8_t, qf[s][c]), sacc[s][blk], 0, 0, 0);
+      }
+    };
+    auto mask1 = [&](int s) __attribute__((always_inline)) {
+      if (masked) {
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            if (kv0 + 32 * blk + 8 * (r >> 2) + 4 * hh + (r & 3) >= p.nkv) sacc[s][blk][r] = -INFINITY;
+      }
+    };
+    auto resc1 = [&](int s) __attribute__((always_inline)) {   // attn_d40_kernel<QS = 1>'s decision, per subtile
+      const float mx = tile_max(sacc[s]);
+      if (first || __any(mx > kRescaleThr)) {
+        const float tgt = mq[s] + mx;
+        const float mn = bf16_rne(first ? tgt : fmaxf(mq[s], tgt));
+        const float delta = mn - mq[s];
+        const float alpha = first ? 0.f : __builtin_amdgcn_exp2f(-delta);
+        mq[s] = mn;
+#pragma unroll
+        for (int db = 0; db < ND32; ++db) oacc[s][db] *= alpha;
+        sacc[s][0] -= delta;
+        sacc[s][1] -= delta;
+        if (hh == (D % 16) / 8) qf[s][D / 16].x = (qf[s][D / 16].x & 0xffff0000u) | (__float_as_uint(-mn) >> 16);
+      }
+    };
+    auto pv1 = [&](int s, const uint4 (&pb)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int db = 0; db < ND32; ++db) {
+        const int cb = 32 * db + 16 * ((lane >> 4) & 1) + 4 * (i16 & 3);
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const T* a0 = Vs + (32 * blk + 16 * st + 4 * hh + (i16 >> 2)) * ROW + cb;
+            const uint2 lo = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0)));
+            const uint2 hi = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t*)(a0 + 8 * ROW)));
+            const uint4 va = make_uint4(lo.x, lo.y, hi.x, hi.y);
+            oacc[s][db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, va),
+                                                                  __builtin_bit_cast(bf16x8_t, pb[blk][st]), oacc[s][db], 0, 0, 0);
+          }
+      }
+    };
+    uint4 pb0[2][2], pb1[2][2];
+    qk1(0);
+    mask1(0);
+    resc1(0);
+    // S(1) beside P(0) (the compiler's interleave: pinning each MFMA to two exps and two other VALU
+    // with sched_group_barrier measured slower, 212.6 -> 235 us at N = 4096)
+    qk1(1);
+    to_p(sacc[0], pb0);
+    // P(0) is consumed here (an empty asm reading it), so the compiler cannot sink its exps below the
+    // rescale branch into the P.V region
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+        asm volatile("" ::"v"(pb0[blk][st].x), "v"(pb0[blk][st].y), "v"(pb0[blk][st].z), "v"(pb0[blk][st].w));
+    mask1(1);
+    resc1(1);
+    // O(0) += V^T P0^T beside P(1)
+    pv1(0, pb0);
+    to_p(sacc[1], pb1);
+    pv1(1, pb1);
+  };
   auto compute = [&](int buf, int kv0, bool masked, bool first, int half) {
+    if constexpr (IL) {
+      compute_il(buf, kv0, masked, first, half);
+      return;
+    }
     f32x16_t sacc[QS][2];
     qk(buf, half, sacc);
     kv0 += 64 * half;
@@ -986,6 +1080,9 @@ __global__ __launch_bounds__(64 * NW, PAIR ? (OCC * NW + 3) / 4 : OCC) void attn
   issue_tile(t0 * KT, bufi(t0));
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+#ifdef ATTN_PRIO   // ablation builds: static priority for the second-dispatched half of the waves
+  if (__builtin_amdgcn_readfirstlane(wave) >= NW / 2) __builtin_amdgcn_s_setprio(1);
+#endif
   if constexpr (!SKEW && PAIR) {
     // tile t in buffer BQ; SURE: tile t + 1 is known to be a full tile
     auto step = [&](int t, auto bq, auto sure) {
@@ -1498,6 +1595,7 @@ int launch_kv_split(const AttnArgs& a, int batch, hipStream_t s) {
 }
 
 int g_attn_skew = 0;     // tuning / A-B hook (ldm_attention_set_skew): 0 planner, 1 off, 2 on
+int g_attn_il = 1;       // A/B hook (ldm_attention_set_il): head_dim 40 two-subtile interleave (IL) where >= 256 blocks
 int g_attn_qs2 = 0;      // tuning / A-B hook: head_dim 40 as 64 queries per wave: 1 two subtiles in step,
                          // 2 the pipelined form (attn_d40p_kernel)
 
@@ -1543,6 +1641,11 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
       } else if (g_attn_qs2 == 1 && g_attn_waves == 0 && nb2 >= 256) {
         // 8 waves x 64 queries (two subtiles sharing every K / V fragment read), one block per CU
         hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 40, 2>), dim3(nb2), dim3(512), 0, s, a);
+      } else if (g_attn_il && g_attn_waves == 0 && g_attn_skew < 2 && nb2 >= 256) {
+        // 8 waves x 64 queries, the two subtiles' MFMA and softmax phases interleaved in each wave
+        // (opbench, graph-replayed, N = 4096 B = 8: 226.0 -> 212.6 us; config 5's N = 2048 B = 16:
+        // 118.4 -> 113.9; with sched_group_barrier-pinned interleaves slower: 235 / 128)
+        hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 40, 2, false, false, false, true>), dim3(nb2), dim3(512), 0, s, a);
       } else if (g_attn_waves == 4) {
         const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
         hipLaunchKernelGGL((attn_d40_kernel<4, 4>), dim3(nb4), dim3(256), 0, s, a);
@@ -2802,6 +2905,7 @@ extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy;
 extern "C" void ldm_attention_set_d80(int enabled) { g_attn_d80 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_d160(int enabled) { g_attn_d160 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_qs2(int mode) { g_attn_qs2 = mode == 1 || mode == 2 ? mode : 0; }
+extern "C" void ldm_attention_set_il(int enabled) { g_attn_il = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_skew(int mode) { g_attn_skew = mode >= 1 && mode <= 3 ? mode : 0; }
 extern "C" void ldm_attention_set_bwd32(int enabled) { g_attn_bwd32 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_maxcol(int mode) {

@@ -126,6 +126,7 @@ EXPORTS = {
     "ldm_attention_force_legacy": (None, [_i]),
     "ldm_attention_set_d80": (None, [_i]),
     "ldm_attention_set_qs2": (None, [_i]),
+    "ldm_attention_set_il": (None, [_i]),
     "ldm_attention_set_skew": (None, [_i]),
     "ldm_attention_set_d160": (None, [_i]),
     "ldm_attention_set_bwd32": (None, [_i]),
@@ -725,6 +726,12 @@ def set_attention_qs2(mode=1):
     blocks per CU); 1 two 32-query subtiles per wave sharing each K / V fragment read (one block per
     CU); 2 the tile loop software-pipelined inside each wave (attn_d40p_kernel)."""
     load_library().ldm_attention_set_qs2(int(mode))
+
+
+def set_attention_il(enabled=True):
+    """A/B hook for head_dim 40 with >= 256 blocks of 64 queries: the two-subtile kernel whose MFMA and
+    softmax phases interleave inside each wave (default on) or the 32-query kernel; bit-identical."""
+    load_library().ldm_attention_set_il(int(bool(enabled)))
 
 
 def set_attention_skew(mode=0):
