@@ -43,6 +43,21 @@ def conv_case(B, H, W, Cin, Cout, k=3, stride=1, up=False, layout=K.OUT_NHWC, ge
     return run, flops, None
 
 
+def ln_gemm_case(rows, C, N, geglu=False):
+    """A LayerNorm-folded 1x1 GEMM as the transformer runs it (norm1 -> QKV, norm3 -> GEGLU): the packed
+    W diag(gamma) weight, the producer's fp64 row statistics."""
+    rows = max(1, rows * BATCH // 8)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(rows, C, device=DEV, generator=g).to(BF)
+    w = torch.randn(N, C, device=DEV, generator=g) * 0.05
+    pc = K.packed_ln_fold(w, torch.randn(N, device=DEV, generator=g), torch.rand(C, device=DEV, generator=g) + 0.5,
+                          torch.randn(C, device=DEV, generator=g) * 0.1, BF, geglu=geglu)
+    xf = x.double()
+    rs = torch.stack([xf.sum(1), (xf * xf).sum(1)], 1).contiguous()
+    lay = K.OUT_GEGLU if geglu else K.OUT_NHWC
+    return (lambda: K.linear(pc, x, ln=(rs, 1e-5), out_layout=lay)), 2.0 * rows * N * C, None
+
+
 def mm_case(M, K, N):
     """torch.mm (hipBLASLt) on the same GEMM shape: the library reference point, no epilogue."""
     a = torch.randn(M, K, device=DEV).to(BF)
@@ -295,6 +310,10 @@ CASES = {
     "gemm_ff2_1280": lambda: conv_case(8, 64, 64, 1280, 320, k=1, residual=True),
     "gemm_geglu_1280": lambda: conv_case(8, 16, 16, 1280, 10240, k=1, geglu=True),
     "gemm_qkv_640": lambda: conv_case(8, 32, 32, 640, 1920, k=1),
+    "gemm_ln_qkv_640": lambda: ln_gemm_case(8192, 640, 1920),
+    "gemm_ln_geglu_640": lambda: ln_gemm_case(8192, 640, 5120, geglu=True),
+    "gemm_ln_qkv_1280": lambda: ln_gemm_case(2048, 1280, 3840),
+    "gemm_ln_geglu_1280": lambda: ln_gemm_case(2048, 1280, 10240, geglu=True),
     "gemm_geglu_640": lambda: conv_case(8, 32, 32, 640, 5120, k=1, geglu=True),
     "gemm_ff2_2560": lambda: conv_case(8, 32, 32, 2560, 640, k=1, residual=True),
     "gemm_proj_640": lambda: conv_case(8, 32, 32, 640, 640, k=1, residual=True),
