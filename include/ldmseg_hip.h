@@ -248,6 +248,32 @@ int ldm_transformer_in(const ldm_gn_fold* gn, const ldm_conv_params* proj_in, co
 void ldm_transformer_in_set_mode(int mode);
 
 /* ---------------------------------------------------------------------------------------
+ * ldm_conv_in — the UNet's conv_in straight from the sampler's NCHW sources, in one launch.
+ * Replaces: ldm_nchw_to_nhwc([x_t || rgb (|| cond)], trainers_ldm_cond.py:1134-1141) + ldm_conv2d of
+ * the 8 / 12-channel conv_in (unet.py:357, built by modify_encoder :178-233).
+ *   src[i], c[i], src_dtype[i]: up to three NCHW [batch][c_i][height][width] tensors (fp32 or bf16),
+ *     concatenated over channels (<= 16 in all), each value rounded to bf16 as ldm_nchw_to_nhwc stores it;
+ *   w: ldm_conv2d's packed [n][kpad] bf16 weight of the 3x3 conv with 16 (zero-padded) input channels
+ *     (k = (ky, kx, c)), bias [n] fp32; out: NHWC bf16 [batch][height][width][n];
+ *   gn_partial / gn_unit / gn_slots: as ldm_conv2d's (the zeroed fp64 GroupNorm accumulators the
+ *     next ldm_group_norm consumes; each output row adds to slot row % gn_slots), or NULL.
+ * Scope: dtype bf16, width <= 64 and % 16 == 0, n % 64 == 0 and <= 320. */
+typedef struct {
+  const void* src[3];
+  int c[3];
+  int src_dtype[3];
+  int batch, height, width;
+  int dtype;                   /* LDM_BF16 */
+  const void* w;
+  int n, kpad;
+  const float* bias;
+  void* out;
+  double* gn_partial;
+  int gn_unit, gn_slots;
+} ldm_conv_in_params;
+int ldm_conv_in(const ldm_conv_in_params* p, ldm_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
  * ldm_attention — fused multi-head scaled-dot-product attention (online softmax, MFMA).
  * Replaces: diffusers Attention(AttnProcessor) self-attention attn1 (and cross-attention
  * attn2 when not removed, unet.py:83-105): softmax(Q K^T * scale) V per (batch, head).

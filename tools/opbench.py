@@ -58,6 +58,22 @@ def ln_gemm_case(rows, C, N, geglu=False):
     return (lambda: K.linear(pc, x, ln=(rs, 1e-5), out_layout=lay)), 2.0 * rows * N * C, None
 
 
+def conv_in_case(B, H=64, W=64, fused=True, stats=True):
+    """The UNet's conv_in from the sampler's two fp32 NCHW sources: ldm_conv_in, or nchw_to_nhwc +
+    ldm_conv2d (gn_stats on, as the UNet runs it)."""
+    B = max(1, B * BATCH // 8)
+    g = torch.Generator(device=DEV).manual_seed(0)
+    srcs = [torch.randn(B, 4, H, W, device=DEV, generator=g) for _ in range(2)]
+    pc = K.PackedConv(torch.randn(320, 8, 3, 3, device=DEV, generator=g) * 0.1, torch.randn(320, device=DEV), BF,
+                      cin_pad=16)
+
+    def run():
+        if fused:
+            return K.conv_in(pc, srcs, B, H, W, gn_stats=stats)
+        return K.conv2d(pc, K.nchw_to_nhwc(srcs, 16, BF), B, H, W, gn_stats=stats)
+    return run, 2.0 * B * H * W * 320 * 72, None
+
+
 def mm_case(M, K, N):
     """torch.mm (hipBLASLt) on the same GEMM shape: the library reference point, no epilogue."""
     a = torch.randn(M, K, device=DEV).to(BF)
@@ -295,6 +311,10 @@ CASES = {
     "conv3_l2_1280": lambda: conv_case(8, 16, 16, 1280, 1280, temb=True, stats=True),
     "conv3_l3_1280": lambda: conv_case(8, 8, 8, 1280, 1280, temb=True, stats=True),
     "conv_in_16": lambda: conv_case(8, 64, 64, 16, 320, stats=True),
+    "cin_fused": lambda: conv_in_case(8),
+    "cin_two": lambda: conv_in_case(8, fused=False),
+    "cin_fused_nostats": lambda: conv_in_case(8, stats=False),
+    "cin_two_nostats": lambda: conv_in_case(8, fused=False, stats=False),
     "conv_in_16_nostats": lambda: conv_case(8, 64, 64, 16, 320),
     "conv_in_64_nostats": lambda: conv_case(8, 64, 64, 64, 320),
     "gemm_320_k64": lambda: conv_case(8, 64, 64, 64, 320, k=1),

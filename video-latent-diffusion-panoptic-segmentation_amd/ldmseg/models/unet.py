@@ -771,8 +771,11 @@ class UNet(nn.Module):
         with (torch.cuda.stream(side) if side is not None else contextlib.nullcontext()):
             temb_all = self._time_embedding(P, t, B, dt)
         # 3. conv_in (unet.py:357)
-        x = K.nchw_to_nhwc(sources, P["cin_pad"], dt)
-        x = K.conv2d(P["conv_in"], x, B, H, W, gn_stats=True)
+        if self.conv_in_fused and K.conv_in_ok(P["conv_in"], sources, B, H, W):
+            x = K.conv_in(P["conv_in"], sources, B, H, W)                  # gather + conv in one launch
+        else:
+            x = K.nchw_to_nhwc(sources, P["cin_pad"], dt)
+            x = K.conv2d(P["conv_in"], x, B, H, W, gn_stats=True)
         if side is not None:
             main.wait_stream(side)
             temb_all.record_stream(main)
@@ -823,6 +826,15 @@ class UNet(nn.Module):
                                want_eps=False)
         x = K.group_norm(x, B, H * W, G, *P["out_norm"], self.conv_norm_out.eps, K.ACT_SILU)
         return K.conv2d(P["conv_out"], x, B, H, W, out_layout=K.OUT_NCHW)
+
+    @property
+    def conv_in_fused(self):
+        return getattr(self, "_conv_in_fused", True)
+
+    def set_conv_in_fused(self, enabled=True):
+        """bf16: run conv_in as one ldm_conv_in launch straight from the NCHW sources (default on); off
+        runs ldm_nchw_to_nhwc + ldm_conv2d (A/B: same bf16 inputs, the conv within bf16 rounding)."""
+        self._conv_in_fused = bool(enabled)
 
     @property
     def tail_fused(self):

@@ -40,6 +40,12 @@ class ConvParams(ctypes.Structure):
                 ("gn_eps", _f), ("gn_skip_out", _i)]
 
 
+class ConvInParams(ctypes.Structure):
+    _fields_ = [("src", _vp * 3), ("c", _i * 3), ("src_dtype", _i * 3), ("batch", _i), ("height", _i), ("width", _i),
+                ("dtype", _i), ("w", _vp), ("n", _i), ("kpad", _i), ("bias", _vp), ("out", _vp), ("gn_partial", _vp),
+                ("gn_unit", _i), ("gn_slots", _i)]
+
+
 class GnFold(ctypes.Structure):
     _fields_ = [("acc", _vp), ("unit", _i), ("slots", _i), ("groups", _i), ("eps", _f), ("gamma", _vp),
                 ("beta", _vp)]
@@ -81,6 +87,7 @@ EXPORTS = {
     "ldm_conv2d_force_plan": (None, [_i, _i, _i]),
     "ldm_conv2d_describe_plan": (_i, [ctypes.POINTER(ConvParams), ctypes.POINTER(ctypes.c_int)]),
     "ldm_conv2d_gn_fusable": (_i, [ctypes.POINTER(ConvParams)]),
+    "ldm_conv_in": (_i, [ctypes.POINTER(ConvInParams), _vp]),
     "ldm_conv2d_set_gn_fuse_min_blocks": (None, [_i]),
     "ldm_conv2d_force_stages": (None, [_i]),
     "ldm_conv2d_set_raster_group": (None, [_i]),
@@ -1352,6 +1359,49 @@ def nchw_to_nhwc(sources, c_pad, dtype):
     out = torch.empty(B, H, W, c_pad, dtype=dtype, device=srcs[0].device)
     _check(lib.ldm_nchw_to_nhwc(*args, B, H * W, c_pad, _ptr(out), dtype_code(dtype), _stream(srcs[0])),
            "ldm_nchw_to_nhwc")
+    return out
+
+
+CONV_IN_MIN_ROWS = 256    # ldm_conv_in blocks (output rows) below which the two launches are faster
+
+
+def conv_in_ok(pc: PackedConv, sources, batch, h, w):
+    """ldm_conv_in takes this conv_in: bf16 3x3 pack over 16 padded channels, n % 64 == 0 (<= 320),
+    width % 16 == 0 (<= 64), the sources' channels <= 16, and >= 256 output rows (one block each: a
+    single 64x64 frame's 64 blocks lose to the two launches, 16.4 vs 15.1 us; at B = 8 24.6 vs 27.7)."""
+    srcs = [t for t in sources if t is not None]
+    return (pc.dtype == torch.bfloat16 and batch * h >= CONV_IN_MIN_ROWS and pc.ksize == 3 and pc.cin == 16 and pc.n % 64 == 0 and pc.n <= 320
+            and pc.bias is not None and w % 16 == 0 and w <= 64 and 1 <= len(srcs) <= 3
+            and sum(t.shape[1] for t in srcs) <= 16
+            and all(t.dtype in (torch.float32, torch.bfloat16) and t.shape[0] == batch and t.shape[2:] == (h, w)
+                    for t in srcs))
+
+
+def conv_in(pc: PackedConv, sources, batch, h, w, gn_stats=True):
+    """The UNet's conv_in on the channel concatenation of up to three NCHW sources, one launch
+    (ldm_conv_in: replaces nchw_to_nhwc + conv2d).  NHWC bf16 [batch, h, w, n] with the GroupNorm
+    accumulators attached as conv2d(gn_stats=True) attaches them."""
+    lib = load_library()
+    srcs = [t.contiguous() for t in sources if t is not None]
+    _gpu(pc.w, *srcs)
+    out = torch.empty(batch, h, w, pc.n, dtype=torch.bfloat16, device=pc.w.device)
+    part, unit, slots = None, 0, 0
+    if gn_stats and (h * w) % 64 == 0:
+        unit, slots = gn_unit_for(pc.n), gn_slots_for(h * w)
+        part = _gn_accumulators(batch, slots, pc.n // unit, pc.w.device)
+    p = ConvInParams()
+    for i, t in enumerate(srcs):
+        p.src[i], p.c[i], p.src_dtype[i] = _ptr(t), t.shape[1], dtype_code(t.dtype)
+    p.batch, p.height, p.width, p.dtype = batch, h, w, dtype_code(torch.bfloat16)
+    p.w, p.n, p.kpad, p.bias, p.out = _ptr(pc.w), pc.n, pc.kpad, _ptr(pc.bias), _ptr(out)
+    p.gn_partial, p.gn_unit, p.gn_slots = _ptr(part), unit, slots
+    ev = _prof_start()
+    _check(lib.ldm_conv_in(ctypes.byref(p), _stream(pc.w)), "ldm_conv_in")
+    setattr(out, GN_PART_ATTR, part)
+    setattr(out, GN_DONE_ATTR, None)
+    _prof_stop(ev, "igemm", 2.0 * batch * h * w * pc.n * 9 * pc.cin_real,
+               sum(t.numel() * t.element_size() for t in srcs) + pc.w.numel() * 2 + out.numel() * 2,
+               f"conv_in M={batch * h * w} N={pc.n} Cin={pc.cin_real}")
     return out
 
 
