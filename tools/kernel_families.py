@@ -3,7 +3,7 @@ tools/step_trace.py share, so a new kernel cannot be counted by one tool and dro
 
 A family is what one C-ABI call's op-log entry stands for (bench.py writes the op log through
 ldmseg.ops.native's launch profiler):
-  igemm        ldm_conv2d (tile / halo / wide / ring / big / ars kernels), ldm_feedforward,
+  igemm        ldm_conv2d (tile / halo / wide / ring / big / ars kernels), ldm_conv_in, ldm_feedforward,
                ldm_transformer_in, ldm_unet_tail; the split-K reductions attach to the op before them
   attention    ldm_attention(_ws / _fp8); the split-KV merge attaches to the op before it, the fp8
                K/V quantisation to the op after it
@@ -17,7 +17,7 @@ import re
 
 KINDS = [
     ("igemm", r"(igemm_kernel|igemm_big_kernel|conv3_halo_kernel|gemm_ars2?_kernel|gemm_wide_kernel|"
-              r"gemm_ring_kernel)<|feedforward_kernel|transformer_in_kernel|unet_tail_kernel", "p"),
+              r"gemm_ring_kernel|conv_in_kernel)<|feedforward_kernel|transformer_in_kernel|unet_tail_kernel", "p"),
     ("igemm", r"splitk_(epilogue|gn)_kernel<", "post"),
     ("attention", r"attn(32|_d40|_f8)?_kernel<", "p"),
     ("attention", r"attn_kv_combine", "post"),
