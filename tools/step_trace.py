@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-launch breakdown of one graph-replayed denoising step from a rocprofv3 kernel trace.
 
-    python tools/step_trace.py TRACE.csv [--first nchw_to_nhwc_kernel] [--top 40] [--csv OUT]
+    python tools/step_trace.py TRACE.csv [--first REGEX] [--top 40] [--csv OUT]
 
 The bench replays the same HIP graph every step, so the trace holds many copies of one launch
 sequence.  Steps are cut at every launch of ``--first`` (the step's entry kernel); the most
@@ -26,7 +26,8 @@ def short(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--first", default="nchw_to_nhwc_kernel")
+    ap.add_argument("--first", default="conv_in_kernel|nchw_to_nhwc_kernel",
+                    help="regex of the step's entry kernel (ldm_conv_in, or the NCHW gather before conv_in)")
     ap.add_argument("--top", type=int, default=0, help="also list the N longest positions")
     ap.add_argument("--csv", default=None)
     a = ap.parse_args()
@@ -34,7 +35,7 @@ def main():
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     steps, cur = [], None
     for r in rows:
-        if a.first in r["Kernel_Name"]:
+        if re.search(a.first, r["Kernel_Name"]):
             cur = []
             steps.append(cur)
         if cur is not None:
