@@ -25,7 +25,10 @@ import torch  # noqa: E402
 # the op before each case in the B = 8 step (profiles/r08_step_trace.txt): to_out 320 before the
 # 64x64 feed-forward + proj_out; to_out 1280 before the 16x16 LN-folded GEGLU on gemm_wide
 PRODUCER = {"ff_po_l0": "gemm_proj_320", "gemm_ln_geglu_1280": "gemm_proj_1280_l2",
-            "gemm_geglu_1280_l2": "gemm_proj_1280_l2"}
+            "gemm_geglu_1280_l2": "gemm_proj_1280_l2",
+            # the 32x32 level: proj_in -> LN-folded QKV, GEGLU -> FF2, to_out -> GEGLU
+            "gemm_ln_qkv_640": "gemm_proj_640", "gemm_ff2_2560": "gemm_ln_geglu_640",
+            "gemm_ln_geglu_640": "gemm_proj_640", "gemm_proj_640": "gemm_ff2_2560"}
 
 
 def main():
