@@ -331,7 +331,8 @@ void ldm_attention_set_d160(int enabled);
 void ldm_attention_set_qs2(int enabled);
 /* A/B hook: head_dim 40 with >= 256 blocks of 64 queries (the headline's and config 5's top level) on the
  * two-subtile kernel whose subtiles' MFMA and softmax phases interleave inside each wave (1, default),
- * or on the 32-query kernel (0); bit-identical. */
+ * or on the 32-query kernel (0); the interleaved kernel runs 128-key tiles (two 64-key halves per
+ * barrier); 2 / 3: on 64- / 256-key tiles (A/B); all bit-identical. */
 void ldm_attention_set_il(int enabled);
 /* Tuning / A-B hook: the head_dim 40 / 80 kernels with the block's waves in two phases half an
  * iteration apart (the upper half runs softmax + P.V of tile t - 1, then Q.K^T of tile t, beside the

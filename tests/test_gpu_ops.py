@@ -323,8 +323,9 @@ def test_attention_d40_qs2_close_to_default(B, N):
     (the software-pipelined tile loop: the same operations per query, bit-identical), and the default
     two-subtile interleaved kernel (ldm_attention_set_il, each subtile with its own rescale decision:
     the 32-query kernel's arithmetic, bit-identical; taken from 256 blocks, B = 4 / 8 at N = 4096)
-    against the 32-query kernel it replaces.  Ragged N
-    exercises the masked last key tile and the partial query block; N = 197 gives 4 key tiles (the
+    against the 32-query kernel it replaces, on 128-key tiles by default and on 64- / 256-key tiles
+    (one / four 64-key halves per barrier, ldm_attention_set_il(2 / 3): the same halves in the same
+    order, bit-identical).  Ragged N exercises the masked last key tile and the partial query block; N = 197 gives 4 key tiles (the
     pipeline's two-tile unroll with an odd tail)."""
     torch.manual_seed(9)
     C, H = 320, 8
@@ -342,6 +343,9 @@ def test_attention_d40_qs2_close_to_default(B, N):
         K.set_attention_qs2(0)
         K.set_attention_il(True)
         outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, 40, N, N, 3 * C, 3 * C, 3 * C).float())
+        for kt_mode in (2, 3):              # the interleaved kernel on 64- / 256-key tiles (default 128)
+            K.set_attention_il(kt_mode)
+            outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, 40, N, N, 3 * C, 3 * C, 3 * C).float())
     finally:
         K.set_attention_qs2(0)
         K.set_attention_il(True)
@@ -351,6 +355,7 @@ def test_attention_d40_qs2_close_to_default(B, N):
     assert (outs[0] - outs[1]).abs().max().item() < 0.05
     assert torch.equal(outs[0], outs[2])
     assert torch.equal(outs[0], outs[3])
+    assert torch.equal(outs[0], outs[4]) and torch.equal(outs[0], outs[5])
 
 
 @pytest.mark.parametrize("B,N,hd", [(4, 4096, 40), (4, 4096 + 37, 40), (4, 64 * 3 + 5, 40), (4, 64, 40), (4, 40, 40),

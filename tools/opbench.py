@@ -422,6 +422,10 @@ CASES = {
     "attn_c5_2048_d40_skew": lambda: attn_case(16, 2048, 320, skew=2),
     "attn_4096_d40_pipe": lambda: attn_case(8, 4096, 320, qs2=2),
     "attn_4096_d40_noil": lambda: attn_case(8, 4096, 320, il=False),
+    "attn_4096_d40_kt64": lambda: attn_case(8, 4096, 320, il=2),
+    "attn_c5_2048_d40_kt64": lambda: attn_case(16, 2048, 320, il=2),
+    "attn_4096_d40_kt256": lambda: attn_case(8, 4096, 320, il=3),
+    "attn_c5_2048_d40_kt256": lambda: attn_case(16, 2048, 320, il=3),
     "attn_c5_2048_d40_noil": lambda: attn_case(16, 2048, 320, il=False),
     "attn_c5_2048_d40_qs2": lambda: attn_case(16, 2048, 320, qs2=1),
     "attn_c5_2048_d40_pipe": lambda: attn_case(16, 2048, 320, qs2=2),

@@ -739,7 +739,7 @@ __global__ __launch_bounds__(64 * NW, PAIR ? (OCC * NW + 3) / 4 : OCC) void attn
   typedef bf16_t T;
   typedef __attribute__((ext_vector_type(16))) float f32x16_t;
   static_assert(D % 8 == 0, "head dim");
-  static_assert(QS == 1 || (QS == 2 && KT == 64), "query subtiles");
+  static_assert(QS == 1 || (QS == 2 && (KT == 64 || (IL && (KT == 128 || KT == 256)))), "query subtiles");
   constexpr int DQ = (D + 16) / 16 * 16, QC = DQ / 16, ND32 = (D + 32) / 32;
   constexpr int EPC = 8, CPR = (DQ > 32 * ND32 ? DQ : 32 * ND32) / 8, RCH = CPR + 1, ROW = RCH * EPC,
                 TILE = KT * ROW, ES = 2;
@@ -967,6 +967,7 @@ __global__ __launch_bounds__(64 * NW, PAIR ? (OCC * NW + 3) / 4 : OCC) void attn
   };
   static_assert(!IL || (QS == 2 && !SKEW && !KVS && !PAIR), "IL interleaves the two subtiles of the plain loop");
   auto compute_il = [&](int buf, int kv0, bool masked, bool first, int half) {
+    first = first && half == 0;                      // (128-key tiles: the second half is never first)
     const T* Ks = lds + buf * 2 * TILE + half * 64 * ROW;
     const T* Vs = lds + buf * 2 * TILE + TILE + half * 64 * ROW;
     kv0 += 64 * half;
@@ -1646,7 +1647,15 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
         // 8 waves x 64 queries, the two subtiles' MFMA and softmax phases interleaved in each wave
         // (opbench, graph-replayed, N = 4096 B = 8: 226.0 -> 212.6 us; config 5's N = 2048 B = 16:
         // 118.4 -> 113.9; with sched_group_barrier-pinned interleaves slower: 235 / 128)
-        hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 40, 2, false, false, false, true>), dim3(nb2), dim3(512), 0, s, a);
+        // 128-key tiles (two 64-key halves per barrier, bit-identical to 64-key tiles): opbench 212.3 ->
+        // 207.7 us, same-box step 9.123 -> 9.113 ms (another box: 219.3 -> 214.7, 9.420 -> 9.376);
+        // 256-key tiles in between (profiles/r08m/attention_key_tiles.txt).  A/B: 2 = 64, 3 = 256
+        if (g_attn_il == 2)
+          hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 40, 2, false, false, false, true>), dim3(nb2), dim3(512), 0, s, a);
+        else if (g_attn_il == 3)
+          hipLaunchKernelGGL((attn_d40_kernel<8, 1, 256, 40, 2, false, false, false, true>), dim3(nb2), dim3(512), 0, s, a);
+        else
+          hipLaunchKernelGGL((attn_d40_kernel<8, 1, 128, 40, 2, false, false, false, true>), dim3(nb2), dim3(512), 0, s, a);
       } else if (g_attn_waves == 4) {
         const int nb4 = (a.nq + 127) / 128 * a.heads * batch;
         hipLaunchKernelGGL((attn_d40_kernel<4, 4>), dim3(nb4), dim3(256), 0, s, a);
@@ -2906,7 +2915,7 @@ extern "C" void ldm_attention_force_legacy(int legacy) { g_attn_legacy = legacy;
 extern "C" void ldm_attention_set_d80(int enabled) { g_attn_d80 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_d160(int enabled) { g_attn_d160 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_qs2(int mode) { g_attn_qs2 = mode == 1 || mode == 2 ? mode : 0; }
-extern "C" void ldm_attention_set_il(int enabled) { g_attn_il = enabled ? 1 : 0; }
+extern "C" void ldm_attention_set_il(int enabled) { g_attn_il = enabled < 0 ? 0 : enabled > 3 ? 3 : enabled; }
 extern "C" void ldm_attention_set_skew(int mode) { g_attn_skew = mode >= 1 && mode <= 3 ? mode : 0; }
 extern "C" void ldm_attention_set_bwd32(int enabled) { g_attn_bwd32 = enabled ? 1 : 0; }
 extern "C" void ldm_attention_set_maxcol(int mode) {

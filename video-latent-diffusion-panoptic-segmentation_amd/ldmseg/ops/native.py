@@ -737,8 +737,9 @@ def set_attention_qs2(mode=1):
 
 def set_attention_il(enabled=True):
     """A/B hook for head_dim 40 with >= 256 blocks of 64 queries: the two-subtile kernel whose MFMA and
-    softmax phases interleave inside each wave (default on) or the 32-query kernel; bit-identical."""
-    load_library().ldm_attention_set_il(int(bool(enabled)))
+    softmax phases interleave inside each wave (default on) or the 32-query kernel; bit-identical.
+    The interleaved kernel runs 128-key tiles; ``enabled=2`` / ``3``: on 64- / 256-key tiles (A/B)."""
+    load_library().ldm_attention_set_il(int(enabled) if enabled in (2, 3) else int(bool(enabled)))
 
 
 def set_attention_skew(mode=0):
