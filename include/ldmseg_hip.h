@@ -302,7 +302,8 @@ int ldm_attention_ws(const ldm_attn_params* p, void* workspace, int64_t workspac
  * n_kv / 128 splits). */
 void ldm_attention_set_kvsplit(int splits);
 /* Tuning / A-B hook: 1 (default) runs the head_dim-80 32x32x16 kernel with the key-tile loop unrolled
- * by two (compile-time K / V buffer per tile; bit-identical), 0 the one-tile loop. */
+ * by two (compile-time K / V buffer per tile; bit-identical), 0 the one-tile loop; 2 / 3: 128-key
+ * tiles without / with the unrolled loop (A/B). */
 void ldm_attention_set_pair(int enabled);
 /* BASELINE config 5 ("fp8 MFMA attention", pose-conditioned video LDM at T=16): as ldm_attention
  * (bf16 inputs and output).

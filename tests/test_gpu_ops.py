@@ -486,7 +486,9 @@ def test_attention_kvsplit_planner():
 def test_attention_pair_bit_identical(B, N, hd, splits):
     """ldm_attention_set_pair(1) (the head_dim-80 default): the key-tile loop unrolled by two runs the
     same operations in the same order, so output and log-sum-exp are bit-identical to the one-tile
-    loop (odd and even tile counts, ragged tails; at head_dim 40 both settings run one kernel)."""
+    loop (odd and even tile counts, ragged tails; at head_dim 40 both settings run one kernel); modes 2 / 3
+    run 128-key tiles (two 64-key halves per barrier) without / with the unroll: the same halves in the
+    same order, bit-identical too."""
     torch.manual_seed(14)
     H = 8
     C = H * hd
@@ -494,18 +496,18 @@ def test_attention_pair_bit_identical(B, N, hd, splits):
     outs = []
     try:
         K.set_attention_kvsplit(splits)
-        for on in (False, True):
-            K.set_attention_pair(on)
-            outs.append(K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C, 3 * C))
+        for mode in (0, 1, 2, 3):
+            K.set_attention_pair(mode)
+            outs.append([K.attention(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C, 3 * C)])
             if splits == 0:
-                outs.append(K.attention_fwd_lse(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C, 3 * C,
-                                                3 * C)[1])
+                outs[-1].append(K.attention_fwd_lse(qkv, qkv[..., C:], qkv[..., 2 * C:], B, H, hd, N, N, 3 * C,
+                                                    3 * C, 3 * C)[1])
     finally:
         K.set_attention_pair(True)
         K.set_attention_kvsplit(-1)
-    half = len(outs) // 2
-    for a, b in zip(outs[:half], outs[half:]):
-        assert torch.equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 def test_attention_softmax_spike():

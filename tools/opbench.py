@@ -414,6 +414,8 @@ CASES = {
     "attn_4096_d40_noskew": lambda: attn_case(8, 4096, 320, skew=1),
     "attn_1024_d80_nopair": lambda: attn_case(8, 1024, 640, pair=False),
     "attn_1024_d80": lambda: attn_case(8, 1024, 640),
+    "attn_1024_d80_kt128": lambda: attn_case(8, 1024, 640, pair=2),
+    "attn_1024_d80_kt128p": lambda: attn_case(8, 1024, 640, pair=3),
     "attn_4096_d40_skew": lambda: attn_case(8, 4096, 320, skew=2),
     "attn_4096_d40_occ1": lambda: attn_case(8, 4096, 320, skew=3),
     "attn_1024_d80_noskew": lambda: attn_case(8, 1024, 640, skew=1),
@@ -437,6 +439,8 @@ CASES = {
     "attn_1024_d80_legacy": lambda: attn_case(8, 1024, 640, legacy=True),
     "attn_256_d160_legacy": lambda: attn_case(8, 256, 1280, legacy=True),
     "attn_1024_d80": lambda: attn_case(8, 1024, 640),
+    "attn_1024_d80_kt128": lambda: attn_case(8, 1024, 640, pair=2),
+    "attn_1024_d80_kt128p": lambda: attn_case(8, 1024, 640, pair=3),
     "attn_1024_d80_x16": lambda: attn_case(8, 1024, 640, d80=False),
     "attn_4096_d40_w8": lambda: attn_case(8, 4096, 320, waves=8),
     "attn_1024_d80_w8": lambda: attn_case(8, 1024, 640, waves=8),

@@ -1619,6 +1619,10 @@ int launch32_dp(const AttnArgs& a, int batch, hipStream_t s) {
       const int nb8 = (a.nq + 255) / 256 * a.heads * batch;
       if (nb8 >= 256 && g_attn_skew == 2)
         hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80, 1, true>), dim3(nb8), dim3(512), 0, s, a);
+      else if (nb8 >= 256 && g_attn_pair == 2)   // A/B: 128-key tiles
+        hipLaunchKernelGGL((attn_d40_kernel<8, 1, 128, 80, 1>), dim3(nb8), dim3(512), 0, s, a);
+      else if (nb8 >= 256 && g_attn_pair == 3)   // A/B: 128-key tiles, two-tile unrolled loop
+        hipLaunchKernelGGL((attn_d40_kernel<8, 1, 128, 80, 1, false, false, true>), dim3(nb8), dim3(512), 0, s, a);
       else if (nb8 >= 256 && g_attn_pair)
         hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80, 1, false, false, true>), dim3(nb8), dim3(512), 0, s, a);
       else if (nb8 >= 256) hipLaunchKernelGGL((attn_d40_kernel<8, 1, 64, 80>), dim3(nb8), dim3(512), 0, s, a);
@@ -2881,7 +2885,7 @@ extern "C" int ldm_attention_ws(const ldm_attn_params* q, void* workspace, int64
   return launch_kv_split(a, q->batch, s);
 }
 
-extern "C" void ldm_attention_set_pair(int enabled) { g_attn_pair = enabled ? 1 : 0; }
+extern "C" void ldm_attention_set_pair(int enabled) { g_attn_pair = enabled < 0 ? 0 : enabled > 3 ? 3 : enabled; }
 
 extern "C" void ldm_attention_set_kvsplit(int splits) { g_attn_kvsplit = splits < 0 ? -1 : (splits == 1 ? 0 : splits); }
 

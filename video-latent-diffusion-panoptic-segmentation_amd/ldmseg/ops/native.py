@@ -754,8 +754,9 @@ def set_attention_d160(enabled=False):
 
 
 def set_attention_pair(enabled=True):
-    """Tuning / A-B hook: the head_dim 80 kernel's key-tile loop unrolled by two (default; bit-identical)."""
-    load_library().ldm_attention_set_pair(1 if enabled else 0)
+    """Tuning / A-B hook: the head_dim 80 kernel's key-tile loop unrolled by two (default; bit-identical).
+    ``enabled=2`` / ``3``: 128-key tiles without / with the unrolled loop (A/B)."""
+    load_library().ldm_attention_set_pair(int(enabled) if enabled in (2, 3) else (1 if enabled else 0))
 
 
 def set_attention_kvsplit(splits=-1):
